@@ -1,0 +1,240 @@
+"""Movement-primitive math (ProMP / DMP / ProDMP) — TEST INFRASTRUCTURE ONLY.
+
+Restates the published algorithms of the third-party ``mp_pytorch<=0.1.3`` (pyproject.toml:30),
+which is NOT vendored under /root/reference and not installed: numeric parity to mp_pytorch is
+**parity unpinned** (SURVEY.md §8c).  What *is* pinned by the reference's own tests
+(test/test_black_box.py:168-368, test/test_replanning_sequencing.py:64-364) — parameter
+counts, T = round(duration/dt) samples with the t0 sample dropped, flat position after tau
+for the linear phase — is re-checked by tests/test_mp_structure.py.
+
+This module is the *specification* the HIP kernels implement (fgx_kernels.hip) and the CPU
+check they are compared with.  Conventions (reference call sites in brackets):
+
+time grid   absolute step index i >= 0, t_i = i*dt (f64); a plan that starts at env step s0
+            uses rows i = s0+1 .. s0+T  [black_box_wrapper.py:120-128: init_time = s0*dt,
+            set_duration(duration, dt) -> T = round(duration/dt) samples after t0]
+phase       linear: x = clip((t-delay)/tau, 0, 1); exp: x = exp(-alpha_x * max(t-delay, 0)/tau)
+            [factory/phase_generator_factory.py:11-14]
+basis       normalized RBF, centres = phase of linspace(delay, delay+tau, n), bandwidth
+            h_j = bw / (c_{j+1}-c_j)^2 (last repeated), phi_j = exp(-h_j (x-c_j)^2 / 2) / sum;
+            zero padding builds n_b + z_s + z_g RBFs and keeps columns z_s..z_s+n_b-1
+            [factory/basis_generator_factory.py:10-17]
+tables      every table value is computed in f64 and rounded once to f32 (mp_pytorch computes
+            in torch f32 on the CPU; f64-then-round is the deliberate, documented choice)
+ProMP       pos_k[d] = fma-chain_j(Phi[i][j], w[d][j]) with Phi = f32(weights_scale*phi);
+            vel_k = f32(f32(pos_{k+1}-pos_k) / dt32_i), dt32_i = f32(f32(t_{i+1}) - f32(t_i)),
+            vel_{T-1} = vel_{T-2}.  params = w, dof-major (w[d][j] = params[d*n_b + j]).
+DMP         tau^2 y'' = alpha(beta(g-y) - tau y') + f, beta = alpha/4, f = x*phi.w' (w' =
+            f32(w*weights_scale)), semi-implicit Euler in scaled time in f32:
+            acc = alpha*(beta*(g-y) - z) + f_k; z += sdt*acc; y += sdt*z; vel = z/tau;
+            y_0 = f32(q0), z_0 = f32(f32(qd0)*tau).  params = [w (dof-major), g (dof)].
+ProDMP      q(s) = c1 y1(s) + c2 y2(s) + Phi_p(s).[w; g], y1 = exp(-alpha s/2), y2 = s y1,
+            Phi_p/Phi_v from the cumulative-trapezoid variation-of-parameters integrals on the
+            grid s_j = j*dt/tau up to s = 6 (pre_compute_length_factor), looked up at the
+            rounded grid index; (c1, c2) solved from q(s0) = q0, q'(s0) = tau*qd0 (2x2
+            Wronskian).  params = per-dof blocks [w_d (n_b), g_d] (num_basis_g = n_b + 1).
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .fp32 import fma32, fma_chain32
+
+f32 = np.float32
+
+
+@dataclass
+class MPSpec:
+    kind: str = "promp"            # promp | dmp | prodmp
+    dof: int = 2
+    n_basis: int = 5
+    phase: str = "linear"          # linear | exp
+    tau: float = 2.0
+    delay: float = 0.0
+    alpha_phase: float = 3.0
+    bandwidth: float = 3.0
+    zero_start: int = 0
+    zero_goal: int = 0
+    weights_scale: float = 1.0
+    goal_scale: float = 1.0
+    alpha: float = 25.0            # DMP / ProDMP spring constant
+    pc_length: float = 6.0         # ProDMP pre_compute_length_factor
+    dt: float = 0.01
+    duration: float = 2.0
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def T(self):
+        return int(round(self.duration / self.dt))
+
+    @property
+    def n_params(self):
+        if self.kind == "promp":
+            return self.dof * self.n_basis
+        return self.dof * (self.n_basis + 1)
+
+
+# ----------------------------------------------------------------------------- phase / basis
+def phase64(spec, t):
+    lin = np.maximum((np.asarray(t, np.float64) - spec.delay) / spec.tau, 0.0)
+    if spec.phase == "linear":
+        return np.minimum(lin, 1.0)
+    return np.exp(-spec.alpha_phase * lin)
+
+
+def centers64(spec):
+    n = spec.n_basis + spec.zero_start + spec.zero_goal
+    u = np.arange(n, dtype=np.float64) / (n - 1) if n > 1 else np.zeros(1)
+    c = u if spec.phase == "linear" else np.exp(-spec.alpha_phase * u)
+    if n > 1:
+        d = np.empty(n)
+        d[:-1] = c[1:] - c[:-1]
+        d[-1] = d[-2]
+    else:
+        d = np.ones(1)
+    h = spec.bandwidth / (d ** 2)
+    return c, h
+
+
+def _seqsum_last(a):
+    """numpy's reduction order over the last axis for n < 8 is a plain left-to-right loop."""
+    n = a.shape[-1]
+    if n >= 8:
+        return np.sum(a, axis=-1)
+    s = a[..., 0] + 0.0
+    for j in range(1, n):
+        s = s + a[..., j]
+    return s
+
+
+def rbf64(spec, x):
+    """Normalized RBF values in f64, zero-padding columns removed: [..., n_basis]."""
+    c, h = centers64(spec)
+    d = np.asarray(x, np.float64)[..., None] - c
+    e = np.exp((-h) * (d * d) / 2)
+    phi = e / _seqsum_last(e)[..., None]
+    return phi[..., spec.zero_start:spec.zero_start + spec.n_basis]
+
+
+# ----------------------------------------------------------------------------- tables
+def prodmp_fine64(spec, n_rows):
+    """ProDMP precompute on the fine grid s_j = j*dt/tau (f64), rows 0..n_rows-1."""
+    h = spec.dt / spec.tau
+    J = int(round(spec.pc_length / h)) + 1
+    J = max(J, n_rows)
+    s = np.arange(J, dtype=np.float64) * h
+    a = spec.alpha
+    x = np.exp(-spec.alpha_phase * s)                      # exp phase at t = s*tau (+delay)
+    phi = rbf64(spec, x)                                   # [J, nb]
+    e = np.exp(a * s / 2)
+    dp1 = (s * e * x)[:, None] * phi
+    dp2 = (e * x)[:, None] * phi
+    p1 = np.zeros_like(dp1)
+    p2 = np.zeros_like(dp2)
+    for j in range(1, J):                                  # cumulative trapezoid
+        p1[j] = p1[j - 1] + h * (dp1[j - 1] + dp1[j]) / 2
+        p2[j] = p2[j - 1] + h * (dp2[j - 1] + dp2[j]) / 2
+    y1 = np.exp(-a * s / 2)
+    y2 = s * y1
+    dy1 = -a / 2 * y1
+    dy2 = -a / 2 * y2 + y1
+    q1 = (a * s / 2 - 1) * e + 1
+    q2 = a / 2 * (e - 1)
+    pb = np.concatenate([p2 * y2[:, None] - p1 * y1[:, None], (q2 * y2 - q1 * y1)[:, None]], 1)
+    vb = np.concatenate([p2 * dy2[:, None] - p1 * dy1[:, None], (q2 * dy2 - q1 * dy1)[:, None]], 1)
+    return dict(pb=pb[:n_rows], vb=vb[:n_rows], y1=y1[:n_rows], y2=y2[:n_rows],
+                dy1=dy1[:n_rows], dy2=dy2[:n_rows])
+
+
+def build_tables(spec, n_rows):
+    """Shared per-config tables by absolute step index i in [0, n_rows) (all f32)."""
+    i = np.arange(n_rows + 1, dtype=np.float64)
+    t = i * spec.dt
+    if spec.kind == "promp":
+        phi = rbf64(spec, phase64(spec, t[:n_rows]))
+        t32 = t.astype(f32)
+        return dict(phi=(spec.weights_scale * phi).astype(f32),
+                    dt32=(t32[1:] - t32[:-1]).astype(f32))
+    if spec.kind == "dmp":
+        x = phase64(spec, t[:n_rows])
+        psi = (x[:, None] * rbf64(spec, x)).astype(f32)
+        s32 = np.maximum((t - spec.delay) / spec.tau, 0.0).astype(f32)
+        return dict(psi=psi, sdt=(s32[1:] - s32[:-1]).astype(f32))
+    if spec.kind == "prodmp":
+        fine = prodmp_fine64(spec, n_rows)
+        return {k: v.astype(f32) for k, v in fine.items()}
+    raise ValueError(spec.kind)
+
+
+# ----------------------------------------------------------------------------- trajectories
+def split_params(spec, params):
+    p = np.asarray(params, f32).reshape(-1, spec.n_params)
+    nb, D = spec.n_basis, spec.dof
+    if spec.kind == "promp":
+        return p.reshape(-1, D, nb), None
+    if spec.kind == "dmp":
+        return p[:, :D * nb].reshape(-1, D, nb), p[:, D * nb:]
+    blk = p.reshape(-1, D, nb + 1)
+    return blk[:, :, :nb], blk[:, :, nb]
+
+
+def trajectory(spec, tables, params, s0, q0, qd0):
+    """Desired (pos, vel) [N, T, dof] f32 for N envs whose plans start at env steps s0[N].
+
+    q0/qd0 are the env's current (f64) joint state used as initial conditions.
+    """
+    N = np.asarray(params).reshape(-1, spec.n_params).shape[0]
+    s0 = np.broadcast_to(np.asarray(s0, np.int64), (N,))
+    T, D = spec.T, spec.dof
+    rows = s0[:, None] + 1 + np.arange(T)[None, :]                  # [N, T]
+    w, g = split_params(spec, params)
+    tau32 = f32(spec.tau)
+    if spec.kind == "promp":
+        phi = tables["phi"][rows]                                     # [N, T, nb]
+        pos = fma_chain32(phi[:, :, None, :], w[:, None, :, :])       # [N, T, D]
+        dt32 = tables["dt32"][rows[:, :-1]][:, :, None]
+        vel = np.empty_like(pos)
+        vel[:, :-1] = (pos[:, 1:] - pos[:, :-1]) / dt32
+        vel[:, -1] = vel[:, -2]
+        return pos, vel
+    if spec.kind == "dmp":
+        ws = (w * f32(spec.weights_scale)).astype(f32)
+        gs = (g * f32(spec.goal_scale)).astype(f32)
+        f = fma_chain32(tables["psi"][rows][:, :, None, :], ws[:, None, :, :])    # [N, T, D]
+        sdt = tables["sdt"][rows]                                     # [N, T]
+        alpha, beta = f32(spec.alpha), f32(spec.alpha / 4)
+        y = np.asarray(q0, np.float64).reshape(N, D).astype(f32)
+        z = (np.asarray(qd0, np.float64).reshape(N, D).astype(f32) * tau32).astype(f32)
+        pos = np.empty((N, T, D), f32)
+        vel = np.empty((N, T, D), f32)
+        for k in range(T):
+            pos[:, k], vel[:, k] = y, z / tau32
+            if k == T - 1:
+                break
+            acc = alpha * (beta * (gs - y) - z) + f[:, k]
+            z = z + sdt[:, k, None] * acc
+            y = y + sdt[:, k, None] * z
+        return pos, vel
+    if spec.kind == "prodmp":
+        ws = (w * f32(spec.weights_scale)).astype(f32)
+        gs = (g * f32(spec.goal_scale)).astype(f32)
+        wg = np.concatenate([ws, gs[:, :, None]], axis=2)             # [N, D, nb+1]
+        tb = tables
+        b = s0
+        y1b, y2b, dy1b, dy2b = tb["y1"][b], tb["y2"][b], tb["dy1"][b], tb["dy2"][b]
+        det = (y1b * dy2b - y2b * dy1b).astype(f32)
+        P = fma_chain32(tb["pb"][b][:, None, :], wg)                  # [N, D]
+        V = fma_chain32(tb["vb"][b][:, None, :], wg)
+        q0f = np.asarray(q0, np.float64).reshape(N, D).astype(f32)
+        v0f = np.asarray(qd0, np.float64).reshape(N, D).astype(f32)
+        A = q0f - P
+        B = (v0f * tau32).astype(f32) - V
+        c1 = ((dy2b[:, None] * A - y2b[:, None] * B) / det[:, None]).astype(f32)
+        c2 = ((y1b[:, None] * B - dy1b[:, None] * A) / det[:, None]).astype(f32)
+        coef = np.concatenate([wg, c1[:, :, None], c2[:, :, None]], axis=2)    # [N, D, nb+3]
+        Hp = np.concatenate([tb["pb"][rows], tb["y1"][rows][..., None], tb["y2"][rows][..., None]], 2)
+        Hv = np.concatenate([tb["vb"][rows], tb["dy1"][rows][..., None], tb["dy2"][rows][..., None]], 2)
+        pos = fma_chain32(Hp[:, :, None, :], coef[:, None, :, :])
+        vel = (fma_chain32(Hv[:, :, None, :], coef[:, None, :, :]) / tau32).astype(f32)
+        return pos, vel
+    raise ValueError(spec.kind)

@@ -1,0 +1,85 @@
+"""The vectorised oracle (oracle/batched.py) is bit-exact with the per-env port and the goldens."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import batched, mp, port
+
+CASES = {
+    "bb_simple": ("SimpleReacher", ("pd", 0.6, 0.075), 0),
+    "bb_long": ("LongSimpleReacher", ("pd", 0.6, 0.075), 0),
+    "bb_hole_vel": ("HoleReacher", ("vel",), 0),
+    "bb_hole_pd": ("HoleReacher", ("pd", 1.0, 0.1), 0),
+    "bb_replan": ("SimpleReacher", ("pd", 1.0, 0.1), 25),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_batched_vs_golden(golden_dir, case):
+    g = np.load(os.path.join(golden_dir, case + ".npz"))
+    name, ctrl, replan = CASES[case]
+    E, n_bb = g["ret"].shape
+    P, V = g["pos"], g["vel"]
+
+    def traj(params, s0, q, qd):
+        rows = s0[:, None] + np.arange(200)[None, :]
+        return P[np.arange(E)[:, None], rows], V[np.arange(E)[:, None], rows]
+
+    bb = batched.BatchedBB(name, E, ctrl, traj_fn=traj, replan_period=replan, info_level=2)
+    np.testing.assert_array_equal(bb._reset_idx(list(range(E)), [100 + i for i in range(E)]), g["obs0"])
+    for b in range(n_bb):
+        obs, ret, te, tr, info = bb.step(None)
+        np.testing.assert_array_equal(info["trajectory_length"], g["tlen"][:, b])
+        np.testing.assert_array_equal(te, g["term"][:, b])
+        np.testing.assert_array_equal(tr, g["trunc"][:, b])
+        np.testing.assert_array_equal(ret, g["ret"][:, b])
+        np.testing.assert_array_equal(info["final_obs"], g["obs"][:, b])
+        done = te | tr
+        np.testing.assert_array_equal(obs[done], g["reset_obs"][:, b][done])
+        for i in range(E):
+            L = g["tlen"][i, b]
+            np.testing.assert_array_equal(info["step_actions"][i, :L], g["actions"][i, b, :L])
+            np.testing.assert_array_equal(info["step_observations"][i, :L], g["step_obs"][i, b, :L])
+            np.testing.assert_array_equal(info["step_rewards"][i, :L], g["step_rew"][i, b, :L])
+
+
+MP_CASES = [
+    ("LongSimpleReacher", ("pd", 0.6, 0.075), mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1), 0),
+    ("SimpleReacher", ("pd", 0.6, 0.075), mp.MPSpec("dmp", 2, 5, "exp", 2.0, alpha_phase=2.0, weights_scale=50), 0),
+    ("HoleReacher", ("pd", 1.0, 0.1), mp.MPSpec("prodmp", 5, 5, "exp", 1.5, alpha=10.0), 0),
+    ("HoleReacher", ("vel",), mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1, weights_scale=2), 0),
+    ("SimpleReacher", ("pd", 1.0, 0.1), mp.MPSpec("prodmp", 2, 5, "exp", 1.5, alpha=10.0), 25),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(MP_CASES)))
+def test_batched_vs_port_with_mp(ci):
+    name, ctrl, spec, replan = MP_CASES[ci]
+    E, n_bb = 6, 3 if replan == 0 else 9
+    rng = np.random.default_rng(1234)
+    bb = batched.BatchedBB(name, E, ctrl, mp_spec=spec, replan_period=replan, info_level=2)
+    tables = bb.tables
+    ports = []
+    for i in range(E):
+        env = port.Reacher(name)
+        fn = (lambda env_: (lambda params, t0, cp, cv: tuple(
+            x[0] for x in mp.trajectory(spec, tables, params, int(round(t0 / 0.01)), cp, cv))))(env)
+        c = port.PD(ctrl[1], ctrl[2]) if ctrl[0] == "pd" else port.Vel()
+        ports.append(port.BlackBoxPort(env, fn, c, replan_period=replan))
+    o_b = bb.reset(seed=7)
+    o_p = np.array([p.reset(seed=7 + i) for i, p in enumerate(ports)])
+    np.testing.assert_array_equal(o_b, o_p)
+    for b in range(n_bb):
+        params = rng.standard_normal((E, spec.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = bb.step(params)
+        for i, p in enumerate(ports):
+            o, r, t1, t2, inf = p.step(params[i])
+            assert r == ret[i]
+            assert t1 == te[i] and t2 == tr[i]
+            assert inf["trajectory_length"] == info["trajectory_length"][i]
+            np.testing.assert_array_equal(o, info["final_obs"][i])
+            np.testing.assert_array_equal(inf["positions"], info["positions"][i])
+            np.testing.assert_array_equal(inf["velocities"], info["velocities"][i])
+            if t1 or t2:
+                np.testing.assert_array_equal(p.reset(), obs[i])
