@@ -1,0 +1,183 @@
+"""Benchmark: inner env-steps/s of fancy_ProMP/LongSimpleReacher-v0 black-box steps on MI355X.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--envs ENVS_PER_GPU]
+For N > 1 launch with torch.distributed.run (one process per GPU); env shards are independent
+(weak scaling: ENVS_PER_GPU envs per rank, seeds = global env index), RCCL only gathers the
+final episode returns.  Prints ONE JSON line on rank 0.
+
+A "step" = one BlackBoxWrapper.step for every env (black_box_wrapper.py:170-253): MP trajectory
+(200 samples), PD control, 200 reacher substeps, return, VectorEnv auto-reset.
+The metric counts inner env steps = sum of trajectory_length over envs and steps.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "inner env-steps/sec, ProMP 5-link Reacher, N=65536 envs at 1/2/4/8 MI355X"
+WORKLOAD = "fancy_ProMP/LongSimpleReacher-v0"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VEC_PEAK_TF = 78.6    # MI355X FP64 vector peak (spec; half the 157.3 TF FP32 vector peak)
+
+
+def episode_bytes_per_env(env):
+    """Algorithmic HBM bytes of one k_episode launch per env (info_level 0, autoreset on)."""
+    n, P, out = env.dof, env.n_params, env.out_dim
+    state = 2 * n * 8 + 2 * 8 + 3 * 8 + 3 * 4 + 5 * 8      # q, qd, goal, hole, steps/plans/flags, rng
+    reads = P * 4 + state
+    writes = state + 2 * out * 4 + 8 + 1 + 1 + 4           # state, obs, final_obs, ret, term, trunc, len
+    return reads + writes
+
+
+def cpu_baseline(seconds=12.0, cores=None):
+    """The oracle port (structure-matched per-env Python loop of the reference) on host cores."""
+    import multiprocessing as mp_
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = cores or max(1, min(16, aff))
+    ctx = mp_.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_worker, [(i, seconds) for i in range(cores)])
+        wall = time.perf_counter() - t0
+    steps = sum(r[0] for r in res)
+    return dict(value=steps / wall, unit="inner env-steps/s", cores=cores, kind="port",
+                sample=f"oracle/port.py per-env loop (MP restatement + PD + 200 substeps + autoreset), "
+                       f"{WORKLOAD}, {cores} processes x ~{seconds:.0f}s, {steps} inner steps; "
+                       f"os.cpu_count()={os.cpu_count()}, affinity={aff}")
+
+
+def _cpu_worker(args):
+    wid, seconds = args
+    from oracle import mp, port
+    spec = mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1)
+    tables = mp.build_tables(spec, 202)
+    rng = np.random.default_rng(1234 + wid)
+
+    def traj(params, t0, q, qd):
+        p, v = mp.trajectory(spec, tables, params, int(round(t0 / 0.01)), q, qd)
+        return p[0], v[0]
+    env = port.Reacher("LongSimpleReacher")
+    bb = port.BlackBoxPort(env, traj, port.PD(0.6, 0.075), verbose=2)
+    bb.reset(seed=wid)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, _, te, tr, info = bb.step(rng.standard_normal(spec.n_params, dtype=np.float32))
+        steps += info["trajectory_length"]
+        if te or tr:
+            bb.reset()
+    return steps, time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--env-id", default=WORKLOAD)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import fancy_gym_crowd_amd as fgx
+    N = args.envs
+    env = fgx.make(args.env_id, num_envs=N, device=dev, seed_offset=rank * N)
+    P = env.n_params
+    # MP parameters: default_rng(1234).standard_normal((N_global, P), f32), this rank's rows
+    allp = np.random.default_rng(1234).standard_normal((N * world, P), dtype=np.float32)
+    params = torch.from_numpy(allp[rank * N:(rank + 1) * N]).to(dev)
+    env.reset(seed=0)
+    obs = torch.empty((N, env.out_dim), dtype=torch.float32, device=dev)
+    fobs = torch.empty_like(obs)
+    ret = torch.empty(N, dtype=torch.float64, device=dev)
+    te = torch.empty(N, dtype=torch.uint8, device=dev)
+    tr = torch.empty(N, dtype=torch.uint8, device=dev)
+    tl = torch.empty(N, dtype=torch.int32, device=dev)
+    acc = torch.zeros((), dtype=torch.int64, device=dev)
+
+    for _ in range(args.warmup):
+        env.step_into(params, obs, ret, te, tr, tl, fobs)
+    torch.cuda.synchronize()
+
+    K = args.steps
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev0[k].record()
+        env.step_into(params, obs, ret, te, tr, tl, fobs)
+        ev1[k].record()
+        acc += tl.sum()
+    if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
+        gathered = [torch.empty_like(ret) for _ in range(world)]
+        dist.all_gather(gathered, ret)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    inner_local = int(acc.item())
+    kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([inner_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        inner = int(c.item())
+    else:
+        inner = inner_local
+
+    if rank == 0:
+        value = inner / elapsed
+        bpe = episode_bytes_per_env(env)
+        achieved = bpe * N / (kern_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "inner env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: reset(seed=0) -> env i seeded with its global index; MP params "
+                    "default_rng(1234).standard_normal((N_global, 25), f32)",
+            "config": {"workload": args.env_id, "envs_per_gpu": N, "global_envs": N * world, "T": env.T,
+                       "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_episode", "kernel_ms": kern_ms, "bytes_per_env": bpe},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

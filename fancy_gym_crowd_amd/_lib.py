@@ -1,0 +1,98 @@
+"""ctypes binding of libfgx.so (include/fgx.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be loaded,
+``lib()`` raises.  torch is imported first so that libfgx.so binds to the HIP runtime torch
+already loaded (both carry the SONAME libamdhip64.so.7): device pointers and streams from
+torch are then valid in libfgx.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfgx.so")
+
+FGX_ABI_VERSION = 1
+ENV_SIMPLE, ENV_HOLE = 0, 1
+MP_NONE, MP_PROMP, MP_DMP, MP_PRODMP = 0, 1, 2, 3
+PHASE_LINEAR, PHASE_EXP = 0, 1
+CTRL_PD, CTRL_VEL, CTRL_POS = 0, 1, 2
+ERRORS = {-1: "FGX_E_INVALID", -2: "FGX_E_HIP", -3: "FGX_E_NOMEM", -4: "FGX_E_UNSUPPORTED"}
+
+
+class FgxConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "abi_version", "env_kind", "n_links", "random_start", "allow_self_collision",
+        "allow_wall_collision", "mp_kind", "phase_kind", "n_basis", "zero_start", "zero_goal",
+        "ctrl_kind", "T", "max_episode_steps", "replan_period", "max_planning_times",
+        "condition_on_desired", "time_aware", "return_context", "reserved0")] + [
+        (n, ctypes.c_double) for n in (
+            "dt", "duration", "tau", "delay", "alpha_phase", "bandwidth", "weights_scale",
+            "goal_scale", "alpha", "pc_length", "p_gain", "d_gain", "act_low", "act_high",
+            "hole_width", "hole_depth", "hole_x", "collision_penalty")]
+
+
+class FgxDims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_envs", "dof", "obs_dim", "ctx_dim", "out_obs_dim", "n_params", "T", "table_rows",
+        "table_stride")] + [("reserved", ctypes.c_int32 * 7)]
+
+
+class FgxInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "positions", "velocities", "step_actions", "step_obs", "step_rewards", "is_collided",
+        "is_success", "end_effector", "reward_dist", "reward_ctrl")]
+
+
+EXPORTS = {
+    "fgx_last_error": (ctypes.c_char_p, []),
+    "fgx_abi_version": (ctypes.c_int, []),
+    "fgx_create": (ctypes.c_int, [ctypes.POINTER(FgxConfig), ctypes.c_int64, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_void_p)]),
+    "fgx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fgx_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FgxDims)]),
+    "fgx_reset": (ctypes.c_int, [ctypes.c_void_p] * 5),
+    "fgx_step": (ctypes.c_int, [ctypes.c_void_p] * 9 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
+                                                         ctypes.c_void_p]),
+    "fgx_step_traj": (ctypes.c_int, [ctypes.c_void_p] * 10 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
+                                                               ctypes.c_void_p]),
+    "fgx_trajectory": (ctypes.c_int, [ctypes.c_void_p] * 5),
+    "fgx_step_raw": (ctypes.c_int, [ctypes.c_void_p] * 7 + [ctypes.c_int32, ctypes.c_void_p]),
+    "fgx_get_state": (ctypes.c_int, [ctypes.c_void_p] * 7),
+    "fgx_set_state": (ctypes.c_int, [ctypes.c_void_p] * 7),
+    "fgx_get_tables": (ctypes.c_int, [ctypes.c_void_p] * 3),
+}
+
+_LIB = None
+
+
+class FgxError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load libfgx.so and declare every exported symbol (no GPU needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (bind to torch's HIP runtime, see module docstring)
+    if not os.path.exists(path):
+        raise FgxError(f"libfgx.so not built ({path}); run __graft_entry__.build() — there is no CPU fallback")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fgx_abi_version() != FGX_ABI_VERSION:
+        raise FgxError("libfgx ABI version mismatch")
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = _LIB.fgx_last_error().decode() if _LIB is not None else ""
+        kind = ERRORS.get(rc, str(rc))
+        if rc in (-1, -4):
+            raise ValueError(f"{kind}: {msg}")
+        raise FgxError(f"{kind}: {msg}")
+    return rc

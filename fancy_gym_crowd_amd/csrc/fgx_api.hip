@@ -1,0 +1,427 @@
+// fgx_api.hip — C ABI (include/fgx.h) of the MI355X black-box rollout engine.
+//
+// Host side only does what the reference does once per env construction (make_bb,
+// make_env_helpers.py:68-136): validate and flatten the configuration, allocate the SoA env
+// state, build the basis tables (on the device), then launch kernels on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/fgx.h"
+#include "fgx_kernels.h"
+#include "fgx_aux.h"
+
+using namespace fgx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(FGX_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+struct Handle {
+  fgx_config cfg;
+  DevCfg dc;
+  DevState st;
+  int device;
+  float* tables = nullptr;
+  double* scratch = nullptr;
+  void* state_block = nullptr;
+  int ctx_dim = 0;
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------ dispatch tables
+// Instantiated shapes: n_links in {2, 5}, n_basis = 5 (every registered reacher MP config).
+#define FGX_FOR_NL(X) X(2) X(5)
+
+template <int ENV, int MP, int CTRL, int NL>
+static int launch_episode_nl(const Handle& h, const float* params, const float* dpos, const float* dvel,
+                             const Outputs& o, hipStream_t stream) {
+  const int threads = 256;
+  const int blocks = (int)((h.dc.N + threads - 1) / threads);
+  const size_t lds = (MP == MP_GIVEN) ? 0 : (size_t)h.dc.rows * h.dc.stride * sizeof(float);
+  hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, 5>), dim3(blocks), dim3(threads), lds, stream, h.dc, h.st,
+                     params, dpos, dvel, o);
+  HIP_TRY(hipGetLastError());
+  return FGX_OK;
+}
+
+template <int ENV, int MP, int CTRL>
+static int launch_episode_ctrl(const Handle& h, const float* params, const float* dpos, const float* dvel,
+                               const Outputs& o, hipStream_t stream) {
+#define X(NL) \
+  if (h.dc.nl == NL) return launch_episode_nl<ENV, MP, CTRL, NL>(h, params, dpos, dvel, o, stream);
+  FGX_FOR_NL(X)
+#undef X
+  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+}
+
+template <int ENV, int MP>
+static int launch_episode_mp(const Handle& h, const float* params, const float* dpos, const float* dvel,
+                             const Outputs& o, hipStream_t stream) {
+  switch (h.dc.ctrl) {
+    case CTRL_PD: return launch_episode_ctrl<ENV, MP, CTRL_PD>(h, params, dpos, dvel, o, stream);
+    case CTRL_VEL: return launch_episode_ctrl<ENV, MP, CTRL_VEL>(h, params, dpos, dvel, o, stream);
+    case CTRL_POS: return launch_episode_ctrl<ENV, MP, CTRL_POS>(h, params, dpos, dvel, o, stream);
+  }
+  return fail(FGX_E_INVALID, "bad ctrl_kind");
+}
+
+template <int ENV>
+static int launch_episode_env(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
+                              const Outputs& o, hipStream_t stream) {
+  switch (mp) {
+    case MP_PROMP: return launch_episode_mp<ENV, MP_PROMP>(h, params, dpos, dvel, o, stream);
+    case MP_DMP: return launch_episode_mp<ENV, MP_DMP>(h, params, dpos, dvel, o, stream);
+    case MP_PRODMP: return launch_episode_mp<ENV, MP_PRODMP>(h, params, dpos, dvel, o, stream);
+    case MP_GIVEN: return launch_episode_mp<ENV, MP_GIVEN>(h, params, dpos, dvel, o, stream);
+  }
+  return fail(FGX_E_INVALID, "bad mp kind");
+}
+
+static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
+                          const Outputs& o, hipStream_t stream) {
+  if (h.dc.env == ENV_SIMPLE) return launch_episode_env<ENV_SIMPLE>(h, mp, params, dpos, dvel, o, stream);
+  return launch_episode_env<ENV_HOLE>(h, mp, params, dpos, dvel, o, stream);
+}
+
+static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, float* obs, hipStream_t stream) {
+  const int threads = 256;
+  const int blocks = (int)((h.dc.N + threads - 1) / threads);
+#define X(NL)                                                                                             \
+  if (h.dc.nl == NL) {                                                                                    \
+    hipLaunchKernelGGL((k_reset<NL>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, seeds, mask, obs); \
+    HIP_TRY(hipGetLastError());                                                                           \
+    return FGX_OK;                                                                                        \
+  }
+  FGX_FOR_NL(X)
+#undef X
+  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+}
+
+// ------------------------------------------------------------------------ config -> DevCfg
+static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim) {
+  if (c.abi_version != FGX_ABI_VERSION) return fail(FGX_E_INVALID, "abi_version mismatch");
+  if (N <= 0) return fail(FGX_E_INVALID, "n_envs must be positive");
+  if (c.env_kind != FGX_ENV_SIMPLE && c.env_kind != FGX_ENV_HOLE) return fail(FGX_E_INVALID, "bad env_kind");
+  if (c.n_links < 1 || c.n_links > kMaxLinks) return fail(FGX_E_INVALID, "n_links out of range");
+  if (c.mp_kind < FGX_MP_NONE || c.mp_kind > FGX_MP_PRODMP) return fail(FGX_E_INVALID, "bad mp_kind");
+  if (c.ctrl_kind < FGX_CTRL_PD || c.ctrl_kind > FGX_CTRL_POS) return fail(FGX_E_INVALID, "bad ctrl_kind");
+  if (c.mp_kind != FGX_MP_NONE) {
+    if (c.T <= 0) return fail(FGX_E_INVALID, "T must be positive");
+    if (c.n_basis != 5) return fail(FGX_E_UNSUPPORTED, "n_basis != 5 not instantiated");
+    if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
+    if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
+      return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14
+    if (c.mp_kind == FGX_MP_PRODMP && c.delay != 0.0) return fail(FGX_E_UNSUPPORTED, "prodmp with delay");
+    if (!(c.tau > 0.0) || !(c.dt > 0.0)) return fail(FGX_E_INVALID, "tau/dt must be positive");
+  }
+  if (c.time_aware && c.return_context) return fail(FGX_E_INVALID, "time_aware with context observation");
+  std::memset(&d, 0, sizeof(d));
+  d.N = N;
+  d.env = c.env_kind;
+  d.nl = c.n_links;
+  d.random_start = c.random_start;
+  d.allow_self = c.allow_self_collision;
+  d.allow_wall = c.allow_wall_collision;
+  d.mp = c.mp_kind;
+  d.phase = c.phase_kind;
+  d.nb = c.n_basis;
+  d.zs = c.zero_start;
+  d.zg = c.zero_goal;
+  d.ctrl = c.ctrl_kind;
+  d.T = c.T;
+  d.max_steps = c.max_episode_steps;
+  d.replan = c.replan_period;
+  d.max_plans = c.max_planning_times;
+  d.cond_desired = c.condition_on_desired;
+  d.time_aware = c.time_aware;
+  d.return_context = c.return_context;
+  const int n = c.n_links;
+  d.obs_dim = (c.env_kind == FGX_ENV_SIMPLE) ? 3 * n + 3 : 3 * n + 4;
+  d.full_dim = d.obs_dim + (c.time_aware ? 1 : 0);
+  // context mask (simple_reacher/mp_wrapper.py:32-40, hole_reacher/mp_wrapper.py:36-46)
+  int m = 0;
+  for (int j = 0; j < 3 * n; ++j)
+    if (c.random_start) d.ctx_idx[m++] = j;
+  int p = 3 * n;
+  if (c.env_kind == FGX_ENV_HOLE) {
+    if (std::isnan(c.hole_width)) d.ctx_idx[m++] = p;
+    p += 1;
+  }
+  d.ctx_idx[m++] = p;
+  d.ctx_idx[m++] = p + 1;
+  ctx_dim = m;
+  d.out_dim = c.return_context ? ctx_dim : d.full_dim;
+  d.n_params = (c.mp_kind == FGX_MP_PROMP) ? n * c.n_basis : n * (c.n_basis + 1);
+  if (c.mp_kind == FGX_MP_NONE) d.n_params = 0;
+  const int max_s0 = c.replan_period > 0 ? c.max_episode_steps : 0;
+  d.rows = max_s0 + c.T + 2;
+  if (c.mp_kind == FGX_MP_PRODMP) {
+    d.stride = 2 * (c.n_basis + 1) + 4;
+  } else {
+    d.stride = c.n_basis + 1;
+  }
+  if (c.mp_kind == FGX_MP_NONE) { d.rows = 0; d.stride = 0; }
+  d.rand_width = std::isnan(c.hole_width);
+  d.rand_x = std::isnan(c.hole_x);
+  d.rand_depth = std::isnan(c.hole_depth);
+  d.n_split = (c.T > 128) ? ((c.T / 2) & ~7) : 0;
+  d.dt = c.dt;
+  d.tau = c.tau;
+  d.p_gain = c.p_gain;
+  d.d_gain = c.d_gain;
+  d.act_lo = c.act_low;
+  d.act_hi = c.act_high;
+  d.act_lo32 = (float)c.act_low;
+  d.act_hi32 = (float)c.act_high;
+  d.dt32 = (float)c.dt;
+  d.tau32 = (float)c.tau;
+  d.hole_w0 = c.hole_width;
+  d.hole_d0 = c.hole_depth;
+  d.hole_x0 = c.hole_x;
+  d.penalty = c.collision_penalty;
+  d.weights_scale = c.weights_scale;
+  d.goal_scale = c.goal_scale;
+  d.alpha = c.alpha;
+  d.ws32 = (float)c.weights_scale;
+  d.gs32 = (float)c.goal_scale;
+  d.alpha32 = (float)c.alpha;
+  d.beta32 = (float)(c.alpha / 4);
+  for (int j = 0; j < 100; ++j) d.lin[j] = (double)j * (1.0 / 99.0);   // np.linspace(0, 1, 100)
+  d.lin[99] = 1.0;
+  return FGX_OK;
+}
+
+extern "C" {
+
+const char* fgx_last_error(void) { return g_err.c_str(); }
+
+int fgx_abi_version(void) { return FGX_ABI_VERSION; }
+
+int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle) {
+  if (!cfg || !handle) return fail(FGX_E_INVALID, "null argument");
+  *handle = nullptr;
+  Handle* h = new Handle();
+  h->cfg = *cfg;
+  h->device = device;
+  int rc = build_devcfg(*cfg, n_envs, h->dc, h->ctx_dim);
+  if (rc) { delete h; return rc; }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { delete h; return fail(FGX_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
+  const int64_t N = n_envs;
+  const int nl = cfg->n_links;
+  size_t off = 0;
+  const size_t o_q = off; off = align_up(off + sizeof(double) * nl * N);
+  const size_t o_qd = off; off = align_up(off + sizeof(double) * nl * N);
+  const size_t o_goal = off; off = align_up(off + sizeof(double) * 2 * N);
+  const size_t o_hole = off; off = align_up(off + sizeof(double) * 3 * N);
+  const size_t o_steps = off; off = align_up(off + sizeof(int32_t) * N);
+  const size_t o_plans = off; off = align_up(off + sizeof(int32_t) * N);
+  const size_t o_flags = off; off = align_up(off + sizeof(uint32_t) * N);
+  const size_t o_rng = off; off = align_up(off + sizeof(uint64_t) * 5 * N);
+  const size_t o_cond = off; off = align_up(off + sizeof(float) * 2 * nl * N);
+  const size_t o_seed = off; off = align_up(off + sizeof(uint64_t) * N);
+  const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
+  e = hipMalloc(&h->state_block, off);
+  if (e != hipSuccess) { delete h; return fail(FGX_E_NOMEM, std::string("hipMalloc state: ") + hipGetErrorString(e)); }
+  char* b = (char*)h->state_block;
+  h->st.q = (double*)(b + o_q);
+  h->st.qd = (double*)(b + o_qd);
+  h->st.goal = (double*)(b + o_goal);
+  h->st.hole = (double*)(b + o_hole);
+  h->st.steps = (int32_t*)(b + o_steps);
+  h->st.plans = (int32_t*)(b + o_plans);
+  h->st.flags = (uint32_t*)(b + o_flags);
+  h->st.rng = (uint64_t*)(b + o_rng);
+  h->st.cond = (float*)(b + o_cond);
+  h->tables = (float*)(b + o_tab);
+  h->st.tables = h->tables;
+  (void)hipMemset(h->state_block, 0, off);
+  // basis tables
+  const DevCfg& d = h->dc;
+  if (d.mp == MP_PROMP || d.mp == MP_DMP) {
+    const int thr = 128, blk = (d.rows + thr - 1) / thr;
+    hipLaunchKernelGGL(k_tables_rbf, dim3(blk), dim3(thr), 0, 0, d, cfg->tau, cfg->delay, cfg->alpha_phase,
+                       cfg->bandwidth, h->tables);
+  } else if (d.mp == MP_PRODMP) {
+    e = hipMalloc(&h->scratch, sizeof(double) * d.rows * 2 * d.nb + 64);
+    if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_NOMEM, "hipMalloc scratch"); }
+    hipLaunchKernelGGL(k_tables_prodmp, dim3(1), dim3(256), 0, 0, d, cfg->tau, cfg->alpha_phase, cfg->bandwidth,
+                       h->scratch, h->tables);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("table kernel: ") + hipGetErrorString(e)); }
+  // a deterministic first reset (seed = env index) so that the state is always valid
+  uint64_t* seeds = (uint64_t*)(b + o_seed);
+  {
+    uint64_t* hs = new uint64_t[N];
+    for (int64_t i = 0; i < N; ++i) hs[i] = (uint64_t)i;
+    e = hipMemcpy(seeds, hs, sizeof(uint64_t) * N, hipMemcpyHostToDevice);
+    delete[] hs;
+    if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, "hipMemcpy seeds"); }
+  }
+  rc = launch_reset(*h, seeds, nullptr, nullptr, 0);
+  if (rc) { fgx_destroy(h); return rc; }
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("create sync: ") + hipGetErrorString(e)); }
+  *handle = h;
+  return FGX_OK;
+}
+
+int fgx_destroy(void* handle) {
+  Handle* h = (Handle*)handle;
+  if (!h) return FGX_OK;
+  (void)hipSetDevice(h->device);
+  if (h->state_block) (void)hipFree(h->state_block);
+  if (h->scratch) (void)hipFree(h->scratch);
+  delete h;
+  return FGX_OK;
+}
+
+int fgx_get_dims(void* handle, fgx_dims* out) {
+  Handle* h = (Handle*)handle;
+  if (!h || !out) return fail(FGX_E_INVALID, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  out->n_envs = (int32_t)h->dc.N;
+  out->dof = h->dc.nl;
+  out->obs_dim = h->dc.obs_dim;
+  out->ctx_dim = h->ctx_dim;
+  out->out_obs_dim = h->dc.out_dim;
+  out->n_params = h->dc.n_params;
+  out->T = h->dc.T;
+  out->table_rows = h->dc.rows;
+  out->table_stride = h->dc.stride;
+  return FGX_OK;
+}
+
+int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, float* obs_out, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  return launch_reset(*h, seeds, mask, obs_out, (hipStream_t)stream);
+}
+
+static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, int32_t* tlen, float* fobs,
+                            const fgx_info* info, int32_t autoreset) {
+  Outputs o;
+  std::memset(&o, 0, sizeof(o));
+  o.obs = obs; o.ret = ret; o.term = te; o.trunc = tr; o.tlen = tlen; o.final_obs = fobs;
+  o.autoreset = autoreset;
+  if (info) {
+    o.positions = info->positions;
+    o.velocities = info->velocities;
+    o.step_actions = info->step_actions;
+    o.step_obs = info->step_obs;
+    o.step_rewards = info->step_rewards;
+    o.is_collided = info->is_collided;
+    o.is_success = info->is_success;
+    o.end_effector = info->end_effector;
+    o.reward_dist = info->reward_dist;
+    o.reward_ctrl = info->reward_ctrl;
+  }
+  return o;
+}
+
+int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t* terminated, uint8_t* truncated,
+             int32_t* traj_len, float* final_obs, const fgx_info* info, int32_t autoreset, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  if (h->dc.mp == MP_NONE) return fail(FGX_E_INVALID, "step-based handle: use fgx_step_raw");
+  if (!params || !obs || !ret || !terminated || !truncated || !traj_len) return fail(FGX_E_INVALID, "null output");
+  if (info && ((info->positions == nullptr) != (info->velocities == nullptr)))
+    return fail(FGX_E_INVALID, "positions and velocities must be given together");
+  if (info && ((info->is_collided == nullptr) != (info->is_success == nullptr)))
+    return fail(FGX_E_INVALID, "is_collided and is_success must be given together");
+  if (info && ((info->reward_dist == nullptr) != (info->reward_ctrl == nullptr)))
+    return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
+  Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
+  return launch_episode(*h, h->dc.mp, params, nullptr, nullptr, o, (hipStream_t)stream);
+}
+
+int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, float* obs, double* ret,
+                  uint8_t* terminated, uint8_t* truncated, int32_t* traj_len, float* final_obs, const fgx_info* info,
+                  int32_t autoreset, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  if (!des_pos || !des_vel || !obs || !ret || !terminated || !truncated || !traj_len)
+    return fail(FGX_E_INVALID, "null argument");
+  if (h->dc.T <= 0) return fail(FGX_E_INVALID, "T must be positive");
+  if (info && ((info->is_collided == nullptr) != (info->is_success == nullptr)))
+    return fail(FGX_E_INVALID, "is_collided and is_success must be given together");
+  if (info && ((info->reward_dist == nullptr) != (info->reward_ctrl == nullptr)))
+    return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
+  Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
+  o.positions = nullptr;
+  o.velocities = nullptr;
+  return launch_episode(*h, MP_GIVEN, nullptr, des_pos, des_vel, o, (hipStream_t)stream);
+}
+
+int fgx_trajectory(void* handle, const float* params, float* des_pos, float* des_vel, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  if (!params || !des_pos || !des_vel) return fail(FGX_E_INVALID, "null argument");
+  return launch_trajectory(h->dc, h->st, params, des_pos, des_vel, (hipStream_t)stream, g_err);
+}
+
+int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward, uint8_t* terminated,
+                 uint8_t* truncated, float* final_obs, int32_t autoreset, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  if (!actions || !obs || !reward || !terminated || !truncated) return fail(FGX_E_INVALID, "null argument");
+  const int threads = 256;
+  const int blocks = (int)((h->dc.N + threads - 1) / threads);
+  hipStream_t s = (hipStream_t)stream;
+#define X(NL)                                                                                                  \
+  if (h->dc.nl == NL) {                                                                                        \
+    if (h->dc.env == ENV_SIMPLE)                                                                               \
+      hipLaunchKernelGGL((k_step_raw<ENV_SIMPLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions, \
+                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_step_raw<ENV_HOLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions,   \
+                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+    HIP_TRY(hipGetLastError());                                                                                \
+    return FGX_OK;                                                                                             \
+  }
+  FGX_FOR_NL(X)
+#undef X
+  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+}
+
+int fgx_get_state(void* handle, double* q, double* qd, double* goal, double* hole, int32_t* steps, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  return fgx_transpose_state(h->dc, h->st, q, qd, goal, hole, steps, (hipStream_t)stream, g_err);
+}
+
+int fgx_set_state(void* handle, const double* q, const double* qd, const double* goal, const double* hole,
+                  const int32_t* steps, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  return fgx_untranspose_state(h->dc, h->st, q, qd, goal, hole, steps, (hipStream_t)stream, g_err);
+}
+
+int fgx_get_tables(void* handle, float* out, void* stream) {
+  Handle* h = (Handle*)handle;
+  if (!h || !out) return fail(FGX_E_INVALID, "null argument");
+  const size_t n = (size_t)h->dc.rows * h->dc.stride;
+  if (n) HIP_TRY(hipMemcpyAsync(out, h->tables, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return FGX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,285 @@
+// fgx_device.h — device-side building blocks of the rollout engine (gfx950).
+//
+// Everything here is compiled with -ffp-contract=off: every f64/f32 expression rounds exactly
+// like the reference's numpy expression it restates; fused multiply-adds appear only where
+// they are written explicitly (__builtin_fma / __builtin_fmaf), i.e. the basis contraction
+// (k-ordered f32 fma chain == f32-input MFMA numerics) and the OpenBLAS ddot orderings of
+// np.linalg.norm / np.dot (verified against the reference's goldens).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fgx_rng.h"
+
+namespace fgx {
+
+constexpr int kMaxLinks = 8;
+constexpr int kMaxObs = 3 * kMaxLinks + 5;
+constexpr int kMaxBasis = 16;
+
+enum : int { ENV_SIMPLE = 0, ENV_HOLE = 1 };
+enum : int { MP_NONE = 0, MP_PROMP = 1, MP_DMP = 2, MP_PRODMP = 3, MP_GIVEN = 4 };
+enum : int { CTRL_PD = 0, CTRL_VEL = 1, CTRL_POS = 2 };
+
+// Table layouts (row = absolute env step index i, see oracle/mp.py):
+//   ProMP : [phi_0 .. phi_{nb-1}, dt32]                      stride nb + 1
+//   DMP   : [psi_0 .. psi_{nb-1}, sdt]                       stride nb + 1
+//   ProDMP: [pb_0 .. pb_nb, vb_0 .. vb_nb, y1, y2, dy1, dy2] stride 2 (nb + 1) + 4
+
+// Flat POD copy of the resolved configuration, passed by value to every kernel.
+struct DevCfg {
+  int64_t N;
+  int env, nl, random_start, allow_self, allow_wall;
+  int mp, phase, nb, zs, zg, ctrl, T, max_steps, replan, max_plans, cond_desired, time_aware,
+      return_context;
+  int obs_dim;      // full env observation (3n+3 simple, 3n+4 hole)
+  int full_dim;     // obs_dim + time_aware
+  int out_dim;      // BB observation width (ctx_dim if return_context else full_dim)
+  int n_params, rows, stride;
+  int rand_width, rand_x, rand_depth;
+  int n_split;      // numpy pairwise split point for a T-long return sum (0: none)
+  int ctx_idx[kMaxObs + 1];
+  double dt, tau, p_gain, d_gain, act_lo, act_hi;
+  float act_lo32, act_hi32, dt32, tau32;
+  double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
+  float ws32, gs32, alpha32, beta32;
+  double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
+};
+
+// SoA env state, owned by the handle ([k][N] for per-link arrays).
+struct DevState {
+  double* q;       // [nl][N]
+  double* qd;      // [nl][N]
+  double* goal;    // [2][N]
+  double* hole;    // [3][N]  x, width, depth
+  int32_t* steps;  // [N] env steps since reset (== TimeLimit elapsed == current_traj_steps)
+  int32_t* plans;  // [N] plan_steps (black_box_wrapper.py:88,199)
+  uint32_t* flags; // [N] bit0: qd holds an f32 array (velocity controller), bit1: has condition
+  uint64_t* rng;   // [5][N]  state hi, state lo, inc hi, inc lo, (has_u32 << 32 | u32)
+  float* cond;     // [2][nl][N] condition_on_desired pos / vel
+  const float* tables;
+};
+
+struct Outputs {
+  float* obs;        // [N, out_dim]
+  double* ret;       // [N]
+  uint8_t* term;     // [N]
+  uint8_t* trunc;    // [N]
+  int32_t* tlen;     // [N]
+  float* final_obs;  // [N, out_dim]
+  // info (black_box_wrapper.py:220-249), [N, T, ...]
+  float* positions;
+  float* velocities;
+  double* step_actions;
+  float* step_obs;
+  double* step_rewards;
+  uint8_t* is_collided;
+  uint8_t* is_success;
+  double* end_effector;
+  double* reward_dist;
+  double* reward_ctrl;
+  int autoreset;
+};
+
+// ------------------------------------------------------------------ exact small helpers
+__device__ __forceinline__ double np_max(double x, double lo) { return (x != x) ? x : (x > lo ? x : lo); }
+__device__ __forceinline__ double np_min(double x, double hi) { return (x != x) ? x : (x < hi ? x : hi); }
+__device__ __forceinline__ float np_maxf(float x, float lo) { return (x != x) ? x : (x > lo ? x : lo); }
+__device__ __forceinline__ float np_minf(float x, float hi) { return (x != x) ? x : (x < hi ? x : hi); }
+
+// np.linalg.norm of a 2-vector == sqrt(ddot) == sqrt(fma(y, y, x*x)) (OpenBLAS order)
+__device__ __forceinline__ double norm2(double x, double y) { return __builtin_sqrt(__builtin_fma(y, y, x * x)); }
+
+__device__ __forceinline__ bool ccw(double ax, double ay, double bx, double by, double cx, double cy) {
+  return (cy - ay) * (bx - ax) - (by - ay) * (cx - ax) > 1e-12;   // classic_control/utils.py:1-2
+}
+
+// numpy pairwise summation (np.sum of a length-L f64 vector, L <= 256) done online.
+// Exact for L <= 128 and for L in [2*split .. split + 128] with split = (Tcap/2) & ~7.
+struct PairwiseSum {
+  double a[8], t;       // single-level state (valid for L <= 128)
+  double b[8], u;       // second-half state (t >= split)
+  double first;
+  __device__ __forceinline__ static double comb(const double* r) {
+    return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  }
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.0; b[j] = 0.0; }
+    t = 0.0; u = 0.0; first = 0.0;
+  }
+  __device__ __forceinline__ static void push(double* r, double& tail, int pos, double v) {
+    const int j = pos & 7;
+    // runtime j: select-chain keeps r[] in registers
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q == j) r[q] = (pos < 8) ? v : r[q] + v;
+    if (j == 7) tail = comb(r);
+    else tail = tail + v;
+  }
+  __device__ __forceinline__ void add(int k, double v, int split) {
+    if (k < 128) push(a, t, k, v);
+    if (split > 0 && k >= split) {
+      if (k == split) first = comb(a);
+      push(b, u, k - split, v);
+    }
+  }
+  __device__ __forceinline__ double result(int L, int split) const {
+    if (L <= 128 || split == 0) return t;
+    return first + u;
+  }
+};
+
+// ------------------------------------------------------------------ RNG state load/store
+__device__ __forceinline__ Pcg64 load_rng(const uint64_t* rng, int64_t N, int64_t e) {
+  Pcg64 r;
+  r.state = ((unsigned __int128)rng[e] << 64) | rng[N + e];
+  r.inc = ((unsigned __int128)rng[2 * N + e] << 64) | rng[3 * N + e];
+  const uint64_t b = rng[4 * N + e];
+  r.has_u32 = (uint32_t)(b >> 32);
+  r.u32 = (uint32_t)b;
+  return r;
+}
+
+__device__ __forceinline__ void store_rng(uint64_t* rng, int64_t N, int64_t e, const Pcg64& r) {
+  rng[e] = (uint64_t)(r.state >> 64);
+  rng[N + e] = (uint64_t)r.state;
+  rng[2 * N + e] = (uint64_t)(r.inc >> 64);
+  rng[3 * N + e] = (uint64_t)r.inc;
+  rng[4 * N + e] = ((uint64_t)r.has_u32 << 32) | r.u32;
+}
+
+// ------------------------------------------------------------------ one env in registers
+template <int NL>
+struct Env {
+  double q[NL], qd[NL];
+  double gx, gy;
+  double hx, hw, hd;
+  int steps;
+  uint32_t flags;
+  // forward kinematics (base_reacher.py:95-103): joints[k+1] = cumsum of (cos, sin)(cumsum q)
+  double jx[NL + 1], jy[NL + 1];
+  double c[NL], s[NL];   // cos/sin of the cumulative angles
+
+  __device__ __forceinline__ void fk() {
+    double ang = 0.0, x = 0.0, y = 0.0;
+    jx[0] = 0.0; jy[0] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      ang = (k == 0) ? q[0] : ang + q[k];
+      double sn, cs;
+      sincos(ang, &sn, &cs);
+      c[k] = cs; s[k] = sn;
+      x = (k == 0) ? cs : x + cs;
+      y = (k == 0) ? sn : y + sn;
+      jx[k + 1] = 0.0 + x;
+      jy[k + 1] = 0.0 + y;
+    }
+  }
+
+  // reset draws (simple_reacher.py:46-54,85-96; hole_reacher.py:242-294; base_reacher.py:73-93)
+  __device__ __forceinline__ void first_joint(const DevCfg& cf, Pcg64& r) {
+    if (cf.random_start) {
+      const double lo = M_PI / 4, hi = 3 * M_PI / 4;
+      q[0] = rng_uniform(r, lo, hi);
+    } else {
+      q[0] = (cf.env == ENV_SIMPLE) ? 0.0 : M_PI / 2;
+    }
+#pragma unroll
+    for (int k = 1; k < NL; ++k) q[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) qd[k] = 0.0;
+    steps = 0;
+    flags = 0;
+  }
+
+  __device__ __forceinline__ void goal_sample(Pcg64& r) {
+    const double total = (double)NL;    // np.sum(link_lengths), unit links
+    double g0 = total, g1 = total;
+    while (norm2(g0, g1) >= total) {
+      g0 = rng_uniform(r, -total, total);
+      g1 = rng_uniform(r, -total, total);
+    }
+    gx = g0; gy = g1;
+  }
+
+  __device__ __forceinline__ void hole_sample(const DevCfg& cf, Pcg64& r) {
+    const double w = cf.rand_width ? rng_uniform(r, 0.15, 0.5) : cf.hole_w0;
+    double x;
+    if (cf.rand_x) {
+      const int side = rng_choice_pm1(r);
+      x = (double)side * rng_uniform(r, w / 2, 3.5);
+    } else {
+      x = cf.hole_x0;
+    }
+    const double d = cf.rand_depth ? rng_uniform(r, 1.0, 1.0) : cf.hole_d0;
+    hx = x; hw = w; hd = d;
+    gx = x; gy = -d;
+  }
+
+  // seeded: reseed-only semantics (the discarded pre-seed goal draw has no effect);
+  // unseeded: continue the stream exactly as the reference's reset() does.
+  __device__ __forceinline__ void reset(const DevCfg& cf, Pcg64& r, bool seeded, uint64_t seed) {
+    if (cf.env == ENV_SIMPLE) {
+      if (seeded) {
+        pcg_seed(r, seed);
+        first_joint(cf, r);
+        goal_sample(r);
+        pcg_seed(r, seed);
+        first_joint(cf, r);
+      } else {
+        goal_sample(r);
+        first_joint(cf, r);
+        goal_sample(r);
+        first_joint(cf, r);
+      }
+    } else {
+      if (seeded) pcg_seed(r, seed);
+      hole_sample(cf, r);
+      first_joint(cf, r);
+    }
+    fk();
+  }
+
+  // ---------------------------------------------------------------- collisions (HoleReacher)
+  __device__ __forceinline__ bool self_collision() const {
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      if (q[k] > M_PI || q[k] < -M_PI) return true;   // base_reacher.py:38-39,111
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+#pragma unroll
+      for (int j = i + 2; j < NL; ++j) {
+        const double ax = jx[i], ay = jy[i], bx = jx[i + 1], by = jy[i + 1];
+        const double cx = jx[j], cy = jy[j], dx = jx[j + 1], dy = jy[j + 1];
+        hit |= (ccw(ax, ay, cx, cy, dx, dy) != ccw(bx, by, cx, cy, dx, dy)) &&
+               (ccw(ax, ay, bx, by, cx, cy) != ccw(ax, ay, bx, by, dx, dy));
+      }
+    return hit;
+  }
+
+  // hole_reacher.py:308-361.  Points of link k: p_j = (c_k*lin_j + jx_k, s_k*lin_j + jy_k),
+  // j = 0..99, with p_0 = joint k and p_99 = joint k+1 exactly.  p_j.y is monotone in j
+  // (rounding is monotone), so a link whose two end joints have y >= 0 has no point below the
+  // ground: only links that dip below y = 0 evaluate their 100 points.
+  __device__ __forceinline__ bool wall_collision(const DevCfg& cf) const {
+    const double left = hx - hw / 2, right = hx + hw / 2, nd = -hd;
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const double y0 = jy[k], y1 = jy[k + 1];
+      if (y0 >= 0.0 && y1 >= 0.0 && nd <= 0.0) continue;
+      const double bx = jx[k], by = jy[k], ck = c[k], sk = s[k];
+      for (int j = 0; j < 100; ++j) {
+        const double px = ck * cf.lin[j] + bx;
+        const double py = sk * cf.lin[j] + by;
+        hit |= ((px < left) && (py < 0.0)) || ((px > right) && (py < 0.0)) ||
+               ((px > left) && (px < right) && (py < nd));
+      }
+    }
+    return hit;
+  }
+};
+
+}  // namespace fgx

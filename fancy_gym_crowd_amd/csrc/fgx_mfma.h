@@ -1,0 +1,176 @@
+// fgx_mfma.h — desired trajectories as an f32 MFMA GEMM (v_mfma_f32_32x32x2_f32).
+//
+// For plans that all start at the same step (no replanning) the ProMP / ProDMP trajectory
+// of every env is   Y[k, (e, d)] = sum_j H[k + 1][j] * C[e][d][j]   — a [T x K] basis table
+// times a [K x (N*dof)] coefficient matrix with K = 8 (ProMP: 5 weights + 3 zero pads;
+// ProDMP: 5 weights, goal, c1, c2).  One wave owns 32 envs (the MFMA's 32 columns) and walks
+// the T rows in 32-row tiles; per dof the K = 8 contraction is 4 chained
+// v_mfma_f32_32x32x2_f32, whose numerics are bit-for-bit the k-ordered fmaf chain of the
+// VALU path (cdna_hip_programming.md §3), so k_traj_mfma == k_traj_valu == k_episode.
+//
+// Operand maps (32x32x2 f32): lane l holds A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
+// C/D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5) for accumulator register r.
+// The kernel is bound by writing the [N, T, dof] f32 outputs (arithmetic intensity
+// 2*K flop per 8 output bytes = 2 flop/B), not by the matrix pipe.
+#pragma once
+#include "fgx_kernels.h"
+
+namespace fgx {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MP, int NL>
+__global__ __launch_bounds__(256) void k_traj_mfma(DevCfg c, DevState s, const float* __restrict__ params,
+                                                   float* __restrict__ dpos, float* __restrict__ dvel) {
+  constexpr int NB = 5, K = 8;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t N = c.N;
+  const int64_t e = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 32 + j;
+  const bool valid = e < N;
+  const int64_t ec = valid ? e : (N - 1);
+  const float* tab = s.tables;
+  const int stride = c.stride;
+
+  // ---- per-env coefficients C[d][k] (only the k = 2s + h this lane feeds are kept)
+  float bco[NL][4];
+  if (MP == MP_PROMP) {
+    const float* p = params + ec * c.n_params;
+#pragma unroll
+    for (int d = 0; d < NL; ++d)
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) {
+        const int kk = 2 * sidx + h;
+        bco[d][sidx] = (kk < NB) ? p[d * NB + kk] : 0.0f;
+      }
+  } else {   // ProDMP, bc at step 0 (oracle/mp.py)
+    const float* p = params + ec * c.n_params;
+    const float* rb = tab;   // row 0
+    const float y1 = rb[2 * NB + 2], y2 = rb[2 * NB + 3], dy1 = rb[2 * NB + 4], dy2 = rb[2 * NB + 5];
+    const float det = y1 * dy2 - y2 * dy1;
+#pragma unroll
+    for (int d = 0; d < NL; ++d) {
+      float w[K];
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) w[kk] = p[d * (NB + 1) + kk] * c.ws32;
+      w[NB] = p[d * (NB + 1) + NB] * c.gs32;
+      float P = 0.0f, V = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk <= NB; ++kk) {
+        P = __builtin_fmaf(rb[kk], w[kk], P);
+        V = __builtin_fmaf(rb[NB + 1 + kk], w[kk], V);
+      }
+      const double q0 = s.q[d * N + ec], qd0 = s.qd[d * N + ec];
+      const float A = (float)q0 - P;
+      const float B = (float)qd0 * c.tau32 - V;
+      w[NB + 1] = (dy2 * A - y2 * B) / det;
+      w[NB + 2] = (y1 * B - dy1 * A) / det;
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) bco[d][sidx] = w[2 * sidx + h];
+    }
+  }
+
+  const int T = c.T;
+  for (int tb = 0; tb < T; tb += 32) {
+    // ---- A operands: this lane feeds time row i = j of the tile, k = 2s + h
+    const int kt = tb + j;                       // plan sample index of the row this lane feeds
+    const int ktc = kt < T ? kt : T - 1;
+    const int row = ktc + 1;                     // table row (s0 = 0)
+    float a1[4], a2[4];
+    if (MP == MP_PROMP) {
+      const int row2 = (ktc < T - 1) ? row + 1 : row - 1;
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) {
+        const int kk = 2 * sidx + h;
+        a1[sidx] = (kk < NB) ? tab[(size_t)row * stride + kk] : 0.0f;
+        a2[sidx] = (kk < NB) ? tab[(size_t)row2 * stride + kk] : 0.0f;
+      }
+    } else {
+      const float* r = tab + (size_t)row * stride;
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) {
+        const int kk = 2 * sidx + h;
+        a1[sidx] = (kk <= NB) ? r[kk] : r[2 * NB + 2 + (kk - NB - 1)];
+        a2[sidx] = (kk <= NB) ? r[NB + 1 + kk] : r[2 * NB + 4 + (kk - NB - 1)];
+      }
+    }
+    f32x16 cp[NL], cq[NL];
+#pragma unroll
+    for (int d = 0; d < NL; ++d) {
+      f32x16 z = {0.0f};
+      cp[d] = z;
+      cq[d] = z;
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) {
+        cp[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[sidx], bco[d][sidx], cp[d], 0, 0, 0);
+        cq[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sidx], bco[d][sidx], cq[d], 0, 0, 0);
+      }
+    }
+    // ---- epilogue: lane (j, h) owns env e, rows 8g + 4h + {0..3}, g = 0..3
+    if (valid) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = tb + 8 * g + 4 * h;
+        if (k0 >= T) continue;
+        float pv[4 * NL], vv[4 * NL];
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int reg = 4 * g + r4;
+          const int k = k0 + r4;
+#pragma unroll
+          for (int d = 0; d < NL; ++d) {
+            const float P = cp[d][reg], Q = cq[d][reg];
+            float vel;
+            if (MP == MP_PROMP) {
+              const int kc = k < T ? k : T - 1;
+              if (kc < T - 1) vel = (Q - P) / tab[(size_t)(kc + 1) * stride + NB];
+              else vel = (P - Q) / tab[(size_t)kc * stride + NB];
+            } else {
+              vel = Q / c.tau32;
+            }
+            pv[r4 * NL + d] = P;
+            vv[r4 * NL + d] = vel;
+          }
+        }
+        const int nrow = (T - k0) < 4 ? (T - k0) : 4;
+        float* op = dpos + (e * T + k0) * NL;
+        float* ov = dvel + (e * T + k0) * NL;
+        if (nrow == 4 && ((NL * 4) % 4) == 0) {
+#pragma unroll
+          for (int q4 = 0; q4 < NL; ++q4) {
+            f32x4 x = {pv[4 * q4], pv[4 * q4 + 1], pv[4 * q4 + 2], pv[4 * q4 + 3]};
+            f32x4 y = {vv[4 * q4], vv[4 * q4 + 1], vv[4 * q4 + 2], vv[4 * q4 + 3]};
+            *reinterpret_cast<f32x4*>(op + 4 * q4) = x;
+            *reinterpret_cast<f32x4*>(ov + 4 * q4) = y;
+          }
+        } else {
+          for (int t = 0; t < nrow * NL; ++t) { op[t] = pv[t]; ov[t] = vv[t]; }
+        }
+      }
+    }
+  }
+}
+
+inline int launch_traj_mfma(const DevCfg& c, const DevState& s, const float* params, float* dpos, float* dvel,
+                            hipStream_t stream) {
+  if (c.replan != 0 || c.nb != 5 || c.cond_desired || (c.T % 4) != 0) return 1;   // per-env plan starts: VALU kernel
+  if (((uintptr_t)dpos | (uintptr_t)dvel) & 15) return 1;
+  const int threads = 256;
+  const int64_t groups = (c.N + 31) / 32;
+  const int blocks = (int)((groups + 3) / 4);
+#define X(NL)                                                                                                  \
+  if (c.nl == NL) {                                                                                            \
+    if (c.mp == MP_PROMP)                                                                                      \
+      hipLaunchKernelGGL((k_traj_mfma<MP_PROMP, NL>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_traj_mfma<MP_PRODMP, NL>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel); \
+    return hipGetLastError() == hipSuccess ? 0 : 2;                                                            \
+  }
+  X(2) X(5)
+#undef X
+  return 1;
+}
+
+}  // namespace fgx

@@ -1,0 +1,328 @@
+"""Environment ids, MP configuration merge and flattening to the C-ABI config.
+
+Mirrors (paths relative to /root/reference/fancy_gym):
+  _BB_DEFAULTS                 envs/registry.py:62-129
+  nested_update                envs/registry.py:264-277   (a dict with a '*_type' key replaces)
+  register / upgrade           envs/registry.py:137-220   ('{ns}_{MP}/{name}' ids, registry.py:243)
+  bb_env_constructor           envs/registry.py:280-309   (defaults <- MPWrapper.mp_config <- overrides)
+  make_bb                      utils/make_env_helpers.py:68-136 (duration, tau, TimeAwareObservation)
+  reacher registrations        envs/__init__.py:57-65, 658-666, 682-698
+  MPWrapper.mp_config          simple_reacher/mp_wrapper.py:10-30, hole_reacher/mp_wrapper.py:10-32
+Third-party defaults restated from mp_pytorch<=0.1.3 [EXT-M] (not in the container).
+"""
+import copy
+import math
+from collections.abc import Mapping
+
+import numpy as np
+
+from . import _lib
+
+_BB_DEFAULTS = {
+    'ProMP': {
+        'wrappers': [],
+        'trajectory_generator_kwargs': {'trajectory_generator_type': 'promp'},
+        'phase_generator_kwargs': {'phase_generator_type': 'linear'},
+        'controller_kwargs': {'controller_type': 'motor', 'p_gains': 1.0, 'd_gains': 0.1},
+        'basis_generator_kwargs': {'basis_generator_type': 'zero_rbf', 'num_basis': 5,
+                                   'num_basis_zero_start': 1, 'basis_bandwidth_factor': 3.0},
+        'black_box_kwargs': {},
+    },
+    'DMP': {
+        'wrappers': [],
+        'trajectory_generator_kwargs': {'trajectory_generator_type': 'dmp'},
+        'phase_generator_kwargs': {'phase_generator_type': 'exp'},
+        'controller_kwargs': {'controller_type': 'motor', 'p_gains': 1.0, 'd_gains': 0.1},
+        'basis_generator_kwargs': {'basis_generator_type': 'rbf', 'num_basis': 5},
+        'black_box_kwargs': {},
+    },
+    'ProDMP': {
+        'wrappers': [],
+        'trajectory_generator_kwargs': {'trajectory_generator_type': 'prodmp', 'duration': 2.0,
+                                        'weights_scale': 1.0},
+        'phase_generator_kwargs': {'phase_generator_type': 'exp', 'tau': 1.5},
+        'controller_kwargs': {'controller_type': 'motor', 'p_gains': 1.0, 'd_gains': 0.1},
+        'basis_generator_kwargs': {'basis_generator_type': 'prodmp', 'alpha': 10, 'num_basis': 5},
+        'black_box_kwargs': {},
+    },
+}
+KNOWN_MPS = list(_BB_DEFAULTS.keys())
+
+# mp_pytorch<=0.1.3 constructor defaults [EXT-M]
+_MP_PYTORCH_DEFAULTS = dict(alpha_phase=3.0, delay=0.0, basis_bandwidth_factor=3.0, num_basis_zero_start=2,
+                            num_basis_zero_goal=0, dmp_alpha=25.0, prodmp_alpha=25.0,
+                            pre_compute_length_factor=6.0, weights_scale=1.0, goal_scale=1.0)
+
+
+class EnvSpec:
+    """A registered step-based env (what gym.make('fancy/<Name>-v0') builds)."""
+
+    def __init__(self, id, kind, kwargs, max_episode_steps, mp_config):
+        self.id = id
+        self.kind = kind                      # 'simple' (torque) | 'hole' (direct velocity)
+        self.kwargs = dict(kwargs)
+        self.max_episode_steps = max_episode_steps
+        self.mp_config = mp_config
+
+
+_SIMPLE_MP_CONFIG = {   # simple_reacher/mp_wrapper.py:10-30
+    'ProMP': {'controller_kwargs': {'p_gains': 0.6, 'd_gains': 0.075}},
+    'DMP': {'controller_kwargs': {'p_gains': 0.6, 'd_gains': 0.075},
+            'trajectory_generator_kwargs': {'weights_scale': 50},
+            'phase_generator_kwargs': {'alpha_phase': 2}},
+    'ProDMP': {},
+}
+_HOLE_MP_CONFIG = {     # hole_reacher/mp_wrapper.py:10-32
+    'ProMP': {'controller_kwargs': {'controller_type': 'velocity'},
+              'trajectory_generator_kwargs': {'weights_scale': 2}},
+    'DMP': {'controller_kwargs': {'controller_type': 'velocity'},
+            'trajectory_generator_kwargs': {'weights_scale': 500},
+            'phase_generator_kwargs': {'alpha_phase': 2.5}},
+    'ProDMP': {},
+}
+
+ENV_SPECS = {}
+ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS = {k: [] for k in KNOWN_MPS + ['all']}
+MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS = {}
+
+
+def nested_update(base, update):
+    """registry.py:264-277: a mapping containing any '*_type' key replaces the sub-dict."""
+    if any(item.endswith('_type') for item in update):
+        return update
+    for k, v in update.items():
+        base[k] = nested_update(base.get(k, {}), v) if isinstance(v, Mapping) else v
+    return base
+
+
+def register(id, kind, kwargs, max_episode_steps=200, mp_config=None, add_mp_types=KNOWN_MPS,
+             mp_config_override=None):
+    """Register a step-based reacher id and its '{ns}_{MP}/{name}' black-box ids (registry.py:137-183)."""
+    spec = EnvSpec(id, kind, kwargs, max_episode_steps, mp_config or {})
+    ENV_SPECS[id] = spec
+    upgrade(id, add_mp_types=add_mp_types, mp_config_override=mp_config_override)
+    return spec
+
+
+def upgrade(id, add_mp_types=KNOWN_MPS, base_id=None, mp_config_override=None):
+    """registry.py:186-261."""
+    base_id = base_id or id
+    for mp_type in add_mp_types:
+        assert mp_type in KNOWN_MPS, 'Unknown mp_type'
+        parts = id.split('/')
+        if len(parts) == 1:
+            ns, name = 'gym', parts[0]
+        elif len(parts) == 2:
+            ns, name = parts
+        else:
+            raise ValueError('env id can not contain multiple "/".')
+        p2 = name.split('-')
+        assert len(p2) >= 2 and p2[-1].startswith('v'), 'Malformed env id, must end in -v{int}.'
+        fancy_id = f'{ns}_{mp_type}/{name}'
+        assert fancy_id not in ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS[mp_type], \
+            f'The environment {id} is already registered for {mp_type}.'
+        _BB_IDS[fancy_id] = (base_id, mp_type, copy.deepcopy((mp_config_override or {}).get(mp_type, {})))
+        ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS[mp_type].append(fancy_id)
+        ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS['all'].append(fancy_id)
+        d = MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS.setdefault(ns, {k: [] for k in KNOWN_MPS + ['all']})
+        d[mp_type].append(fancy_id)
+        d['all'].append(fancy_id)
+
+
+_BB_IDS = {}
+
+# envs/__init__.py:57-65, 658-666, 682-698
+register('fancy/SimpleReacher-v0', 'simple', {'n_links': 2}, 200, _SIMPLE_MP_CONFIG)
+register('fancy/LongSimpleReacher-v0', 'simple', {'n_links': 5}, 200, _SIMPLE_MP_CONFIG)
+register('fancy/HoleReacher-v0', 'hole', {'n_links': 5, 'random_start': True, 'allow_self_collision': False,
+                                          'allow_wall_collision': False, 'hole_width': None,
+                                          'hole_depth': 1, 'hole_x': None, 'collision_penalty': 100},
+         200, _HOLE_MP_CONFIG)
+
+
+# --------------------------------------------------------------------------- replanning schedules
+class ReplanEvery:
+    """The data-parallel form of ``replanning_schedule``: replan when the env step t % period == 0
+    (example_replanning_envs.py:37-39).  Callable with the reference's signature."""
+
+    def __init__(self, period):
+        if int(period) <= 0:
+            raise ValueError("period must be positive")
+        self.period = int(period)
+
+    def __call__(self, pos, vel, obs, action, t):
+        return t % self.period == 0
+
+
+def _schedule_period(schedule, max_steps):
+    """Compile a replanning_schedule to an on-device period, or raise (only t % k == 0 is data-parallel)."""
+    if schedule is None:
+        return 0
+    if isinstance(schedule, ReplanEvery):
+        return schedule.period
+    if isinstance(schedule, int):
+        return int(schedule)
+    if not callable(schedule):
+        raise ValueError("replanning_schedule must be callable or an int period")
+    dummy = np.zeros(1)
+    try:
+        hits = [t for t in range(1, max_steps + 1) if bool(schedule(dummy, dummy, dummy, dummy, t))]
+        probe = [t for t in range(1, max_steps + 1) if bool(schedule(dummy + 1.0, dummy - 1.0, dummy + 2.0, dummy + 3.0, t))]
+    except Exception as e:   # state-dependent schedules (crowd_navigation/utils.py:9-10) are not data-parallel
+        raise NotImplementedError(f"replanning_schedule is not a pure function of t: {e}")
+    if hits != probe or not hits:
+        raise NotImplementedError("only schedules of the form t % k == 0 run on the device")
+    k = hits[0]
+    if hits != list(range(k, max_steps + 1, k)):
+        raise NotImplementedError("only schedules of the form t % k == 0 run on the device")
+    return k
+
+
+# --------------------------------------------------------------------------- resolution
+def parse_id(env_id):
+    ns_mp, _, name = env_id.partition('/')
+    if env_id in ENV_SPECS:
+        return env_id, None, {}
+    if env_id not in _BB_IDS:
+        raise ValueError(f"unknown env id {env_id!r}; known: {sorted(list(ENV_SPECS) + list(_BB_IDS))}")
+    base_id, mp_type, reg_override = _BB_IDS[env_id]
+    return base_id, mp_type, reg_override
+
+
+def resolve(env_id, mp_config_override=None, **env_kwargs):
+    """id (+ overrides) -> (fgx_config, meta) exactly as bb_env_constructor + make_bb resolve it."""
+    base_id, mp_type, reg_override = parse_id(env_id)
+    spec = ENV_SPECS[base_id]
+    kw = dict(spec.kwargs)
+    kw.update(env_kwargs)
+    c = _lib.FgxConfig()
+    c.abi_version = _lib.FGX_ABI_VERSION
+    n = int(kw['n_links'])
+    c.n_links = n
+    c.env_kind = _lib.ENV_SIMPLE if spec.kind == 'simple' else _lib.ENV_HOLE
+    rs_default = True if spec.kind == 'simple' else False     # HoleReacherEnv default random_start=False
+    c.random_start = int(bool(kw.get('random_start', rs_default)))
+    c.allow_self_collision = int(bool(kw.get('allow_self_collision', False)))
+    c.allow_wall_collision = int(bool(kw.get('allow_wall_collision', False)))
+    c.dt = 0.01                                                # base_reacher.py:21
+    c.max_episode_steps = int(spec.max_episode_steps)
+    nan = float('nan')
+    if spec.kind == 'hole':
+        c.hole_width = nan if kw.get('hole_width', 1.0) is None else float(kw.get('hole_width', 1.0))
+        c.hole_depth = nan if kw.get('hole_depth') is None else float(kw['hole_depth'])
+        c.hole_x = nan if kw.get('hole_x') is None else float(kw['hole_x'])
+        c.collision_penalty = float(kw.get('collision_penalty', 1000))
+        bound = float(np.float32(2 * np.pi))                   # Box(float32) bounds, base_reacher_direct.py:16-18
+        if kw.get('rew_fct', 'simple') != 'simple':
+            raise NotImplementedError("HoleReacher rew_fct other than 'simple' (hr_simple_reward.py)")
+    else:
+        c.hole_width = c.hole_depth = c.hole_x = nan
+        bound = 1000.0                                          # base_reacher_torque.py:16-18
+        if kw.get('target') is not None:
+            raise NotImplementedError("SimpleReacher with a fixed target")
+    c.act_low, c.act_high = -bound, bound
+    meta = dict(env_id=env_id, base_id=base_id, mp_type=mp_type, kind=spec.kind, n_links=n,
+                reward_aggregation='sum', verbose=1)
+    if mp_type is None:                                          # step-based env
+        c.mp_kind = _lib.MP_NONE
+        c.T = 1
+        c.return_context = 0
+        return c, meta
+
+    # ---- bb_env_constructor (registry.py:280-309)
+    mp_config = spec.mp_config
+    active = copy.deepcopy(mp_config.get(mp_type, {}))
+    inherit = active.pop('inherit_defaults', mp_config.get('inherit_defaults', True))
+    config = copy.deepcopy(_BB_DEFAULTS[mp_type]) if inherit else {}
+    config = nested_update(config, active)
+    config = nested_update(config, copy.deepcopy(reg_override))
+    config = nested_update(config, copy.deepcopy(mp_config_override or {}))
+    wrappers = config.pop('wrappers', [])
+    tg = config.pop('trajectory_generator_kwargs', {})
+    bb = config.pop('black_box_kwargs', {})
+    ctrl = config.pop('controller_kwargs', {})
+    ph = config.pop('phase_generator_kwargs', {})
+    bs = config.pop('basis_generator_kwargs', {})
+
+    # ---- make_bb (make_env_helpers.py:68-136)
+    if bb.get('learn_sub_trajectories') and bb.get('replanning_schedule'):
+        raise ValueError('Cannot used sub-trajectory learning and replanning together.')
+    if bb.get('learn_sub_trajectories'):
+        raise NotImplementedError("learn_sub_trajectories (per-env tau) is not implemented on the device yet")
+    if ph.get('learn_tau') or ph.get('learn_delay'):
+        raise NotImplementedError("learn_tau / learn_delay (per-env phase) are not implemented on the device yet")
+    duration = bb.get('duration')
+    if duration is None:
+        duration = c.max_episode_steps * c.dt
+    if tg.get('duration') is not None and bb.get('time_limit') is not None:
+        assert tg['duration'] == bb['time_limit']
+    tau = ph.get('tau', duration)
+    if tau is None:
+        tau = duration
+    action_dim = int(tg.get('action_dim', n))
+    if action_dim != n:
+        raise ValueError("action_dim must equal n_links for the reacher envs")
+    period = _schedule_period(bb.get('replanning_schedule'), c.max_episode_steps)
+    time_aware = period > 0 or any(getattr(w, '__name__', '') == 'TimeAwareObservation' for w in wrappers)
+
+    tg_type = tg.get('trajectory_generator_type', '').lower()
+    ph_type = ph.get('phase_generator_type', '').lower()
+    bs_type = bs.get('basis_generator_type', '').lower()
+    ct_type = ctrl.get('controller_type', '').lower()
+    c.mp_kind = {'promp': _lib.MP_PROMP, 'dmp': _lib.MP_DMP, 'prodmp': _lib.MP_PRODMP}.get(tg_type, -1)
+    if c.mp_kind < 0:
+        raise ValueError(f"Specified movement primitive type {tg_type} not supported")
+    c.phase_kind = {'linear': _lib.PHASE_LINEAR, 'exp': _lib.PHASE_EXP}.get(ph_type, -1)
+    if c.phase_kind < 0:
+        raise ValueError(f"Specified phase generator type {ph_type} not supported")
+    if bs_type not in ('rbf', 'zero_rbf', 'prodmp'):
+        raise ValueError(f"Specified basis generator type {bs_type} not supported")
+    if bs_type == 'prodmp' and ph_type != 'exp':
+        raise AssertionError("ProDMP basis needs the exp phase generator")
+    if (tg_type == 'prodmp') != (bs_type == 'prodmp'):
+        raise AssertionError("prodmp trajectory generator needs the prodmp basis generator")
+    c.ctrl_kind = {'motor': _lib.CTRL_PD, 'velocity': _lib.CTRL_VEL, 'position': _lib.CTRL_POS}.get(ct_type, -1)
+    if c.ctrl_kind < 0:
+        raise ValueError(f"Specified controller type {ct_type} not supported")
+    D = _MP_PYTORCH_DEFAULTS
+    c.n_basis = int(bs.get('num_basis', 10))
+    c.zero_start = int(bs.get('num_basis_zero_start', D['num_basis_zero_start'])) if bs_type == 'zero_rbf' else 0
+    c.zero_goal = int(bs.get('num_basis_zero_goal', D['num_basis_zero_goal'])) if bs_type == 'zero_rbf' else 0
+    if int(bs.get('num_basis_outside', 0)) != 0:
+        raise NotImplementedError("num_basis_outside != 0")
+    c.bandwidth = float(bs.get('basis_bandwidth_factor', D['basis_bandwidth_factor']))
+    c.tau = float(tau)
+    c.delay = float(ph.get('delay', D['delay']))
+    c.alpha_phase = float(ph.get('alpha_phase', D['alpha_phase']))
+    c.weights_scale = float(tg.get('weights_scale', D['weights_scale']))
+    c.goal_scale = float(tg.get('goal_scale', D['goal_scale']))
+    if tg_type == 'prodmp':
+        c.alpha = float(bs.get('alpha', D['prodmp_alpha']))
+        c.pc_length = float(bs.get('pre_compute_length_factor', D['pre_compute_length_factor']))
+        if float(bs.get('dt', c.dt)) != c.dt:
+            raise NotImplementedError("ProDMP basis dt different from the env dt")
+    else:
+        c.alpha = float(tg.get('alpha', D['dmp_alpha']))
+        c.pc_length = D['pre_compute_length_factor']
+    c.p_gain = float(ctrl.get('p_gains', 1.0))
+    c.d_gain = float(ctrl.get('d_gains', 0.5))
+    if np.ndim(ctrl.get('p_gains', 1.0)) or np.ndim(ctrl.get('d_gains', 0.5)):
+        raise NotImplementedError("per-joint PD gains")
+    c.T = int(round(duration / c.dt))
+    c.duration = float(duration)
+    c.replan_period = int(period)
+    mpt = bb.get('max_planning_times', math.inf)
+    c.max_planning_times = 0 if mpt is None or mpt == math.inf else int(mpt)
+    c.condition_on_desired = int(bool(bb.get('condition_on_desired', False)))
+    c.time_aware = int(time_aware)
+    c.return_context = int(not (period > 0 or bb.get('learn_sub_trajectories')))
+    agg = bb.get('reward_aggregation', np.sum)
+    if agg is np.sum:
+        meta['reward_aggregation'] = 'sum'
+    elif agg is np.mean:
+        meta['reward_aggregation'] = 'mean'
+    else:
+        raise NotImplementedError("reward_aggregation other than np.sum / np.mean")
+    meta['verbose'] = int(bb.get('verbose', 1))
+    meta['n_params'] = n * c.n_basis + (0 if tg_type == 'promp' else n)
+    return c, meta

@@ -1,0 +1,331 @@
+"""Batched black-box / step-based reacher envs on one MI355X, returning torch-ROCm tensors.
+
+The Python surface mirrors what a user of the reference gets from
+``gymnasium.vector.SyncVectorEnv([lambda: gym.make('fancy_ProMP/...')] * N)``:
+  reset(seed, options) -> (obs [N, obs_dim] f32, info)          (black_box_wrapper.py:258-267)
+  step(actions)        -> (obs, reward [N] f64, terminated [N] bool, truncated [N] bool, info)
+                                                                  (black_box_wrapper.py:170-253)
+with gymnasium 0.29 vector semantics [EXT-M]: reset(seed=s) seeds env i with s + i; finished
+envs are auto-reset inside step() and their last observation is in
+info['final_observation'] with the boolean mask info['_final_observation'].
+
+All compute runs in libfgx.so (HIP) on the tensors' device; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .registry import resolve
+
+
+class Box:
+    """Minimal gymnasium.spaces.Box stand-in (bounds in the space dtype, as gymnasium stores them)."""
+
+    def __init__(self, low, high, shape=None, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        shape = tuple(shape) if shape is not None else np.shape(low)
+        self.shape = shape
+        self.low = np.broadcast_to(np.asarray(low, float), shape).astype(self.dtype)
+        self.high = np.broadcast_to(np.asarray(high, float), shape).astype(self.dtype)
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        lo, hi = self.low.astype(float), self.high.astype(float)
+        out = np.where(np.isfinite(lo) & np.isfinite(hi), rng.uniform(np.nan_to_num(lo), np.nan_to_num(hi)),
+                       rng.standard_normal(self.shape))
+        return out.astype(self.dtype)
+
+    def __repr__(self):
+        return f"Box({self.shape}, {self.dtype})"
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _Engine:
+    """Owns one libfgx handle (one device)."""
+
+    def __init__(self, cfg, num_envs, device):
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("fancy_gym_crowd_amd runs on a ROCm GPU device (cuda:N); there is no CPU path")
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        torch.cuda.set_device(idx)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.fgx_create(ctypes.byref(cfg), int(num_envs), int(idx), ctypes.byref(h)))
+        self.h = h
+        d = _lib.FgxDims()
+        _lib.check(self.lib.fgx_get_dims(h, ctypes.byref(d)))
+        self.dims = d
+
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.fgx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BlackBoxVectorEnv:
+    """N black-box envs (one BB step = one whole (sub-)episode) on one GPU."""
+
+    def __init__(self, env_id, num_envs, device="cuda", mp_config_override=None, info_level=None,
+                 autoreset=True, seed_offset=0, **env_kwargs):
+        cfg, meta = resolve(env_id, mp_config_override, **env_kwargs)
+        if meta["mp_type"] is None:
+            raise ValueError(f"{env_id} is a step-based id; use StepVectorEnv / make()")
+        self.meta = meta
+        self.num_envs = int(num_envs)
+        self.info_level = meta["verbose"] if info_level is None else int(info_level)
+        self.autoreset = bool(autoreset)
+        self.seed_offset = int(seed_offset)
+        self._eng = _Engine(cfg, num_envs, device)
+        d = self._eng.dims
+        self.dof, self.T, self.n_params = d.dof, d.T, d.n_params
+        self.obs_dim, self.out_dim, self.full_dim = d.obs_dim, d.out_obs_dim, d.obs_dim + cfg.time_aware
+        self.device = self._eng.device
+        self.single_action_space = Box(-np.inf, np.inf, (self.n_params,), np.float32)
+        self.action_space = Box(-np.inf, np.inf, (self.num_envs, self.n_params), np.float32)
+        self.single_observation_space = self._obs_space(cfg)
+        self.observation_space = Box(np.broadcast_to(self.single_observation_space.low, (self.num_envs, self.out_dim)),
+                                     np.broadcast_to(self.single_observation_space.high, (self.num_envs, self.out_dim)))
+        self._alloc()
+
+    def _obs_space(self, cfg):
+        n = self.dof
+        if cfg.env_kind == _lib.ENV_SIMPLE:
+            bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf] * 2, [np.inf]])
+        else:
+            bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf], [np.inf] * 2, [np.inf]])
+        low, high = -bound, bound
+        if cfg.time_aware:
+            low, high = np.append(low, 0.0), np.append(high, 1.0)
+        if cfg.return_context:
+            rs = [bool(cfg.random_start)] * (3 * n)
+            mask = rs + ([math_isnan(cfg.hole_width)] if cfg.env_kind == _lib.ENV_HOLE else []) + [True, True, False]
+            low, high = low[np.array(mask)], high[np.array(mask)]
+        return Box(low, high, dtype=np.float32)
+
+    def _alloc(self):
+        N, dev = self.num_envs, self.device
+        self._obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=dev)
+        self._fobs = torch.empty((N, self.out_dim), dtype=torch.float32, device=dev)
+        self._ret = torch.empty(N, dtype=torch.float64, device=dev)
+        self._te = torch.empty(N, dtype=torch.uint8, device=dev)
+        self._tr = torch.empty(N, dtype=torch.uint8, device=dev)
+        self._len = torch.empty(N, dtype=torch.int32, device=dev)
+
+    # ------------------------------------------------------------------ gymnasium-style API
+    def reset(self, *, seed=None, options=None):
+        N = self.num_envs
+        obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
+        seeds = None
+        if seed is not None:
+            if isinstance(seed, (list, tuple, np.ndarray, torch.Tensor)):
+                s = torch.as_tensor(np.asarray(seed, dtype=np.uint64).astype(np.int64), device=self.device)
+            else:
+                s = torch.arange(N, dtype=torch.int64, device=self.device) + (int(seed) + self.seed_offset)
+            seeds = s.contiguous()
+        mask = None
+        if options and options.get("reset_mask") is not None:
+            mask = torch.as_tensor(options["reset_mask"], dtype=torch.uint8, device=self.device).contiguous()
+        _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), _ptr(mask), _ptr(obs), self._eng.stream()))
+        return obs, {}
+
+    def _info_buffers(self):
+        if self.info_level < 2:
+            return None, {}
+        N, T, n, dev = self.num_envs, self.T, self.dof, self.device
+        b = dict(positions=torch.full((N, T, n), float("nan"), dtype=torch.float32, device=dev),
+                 velocities=torch.full((N, T, n), float("nan"), dtype=torch.float32, device=dev),
+                 step_actions=torch.full((N, T, n), float("nan"), dtype=torch.float64, device=dev),
+                 step_observations=torch.full((N, T, self.full_dim), float("nan"), dtype=torch.float32, device=dev),
+                 step_rewards=torch.full((N, T), float("nan"), dtype=torch.float64, device=dev))
+        info = _lib.FgxInfo()
+        info.positions, info.velocities = b["positions"].data_ptr(), b["velocities"].data_ptr()
+        info.step_actions, info.step_obs = b["step_actions"].data_ptr(), b["step_observations"].data_ptr()
+        info.step_rewards = b["step_rewards"].data_ptr()
+        if self.meta["kind"] == "hole":
+            b["is_collided"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
+            b["is_success"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
+            b["end_effector"] = torch.full((N, T, 2), float("nan"), dtype=torch.float64, device=dev)
+            info.is_collided, info.is_success = b["is_collided"].data_ptr(), b["is_success"].data_ptr()
+            info.end_effector = b["end_effector"].data_ptr()
+        else:
+            b["reward_dist"] = torch.full((N, T), float("nan"), dtype=torch.float64, device=dev)
+            b["reward_ctrl"] = torch.full((N, T), float("nan"), dtype=torch.float64, device=dev)
+            info.reward_dist, info.reward_ctrl = b["reward_dist"].data_ptr(), b["reward_ctrl"].data_ptr()
+        return info, b
+
+    def _check_actions(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32:
+            a = a.to(torch.float32)
+        if tuple(a.shape) != (self.num_envs, self.n_params):
+            raise ValueError(f"actions must have shape {(self.num_envs, self.n_params)}, got {tuple(a.shape)}")
+        return a.contiguous()
+
+    def step(self, actions):
+        a = self._check_actions(actions)
+        N = self.num_envs
+        obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
+        fobs = torch.empty_like(obs)
+        ret = torch.empty(N, dtype=torch.float64, device=self.device)
+        te = torch.empty(N, dtype=torch.uint8, device=self.device)
+        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        tl = torch.empty(N, dtype=torch.int32, device=self.device)
+        info_s, bufs = self._info_buffers()
+        _lib.check(self._eng.lib.fgx_step(self._eng.h, _ptr(a), _ptr(obs), _ptr(ret), _ptr(te), _ptr(tr), _ptr(tl),
+                                          _ptr(fobs), ctypes.byref(info_s) if info_s is not None else None,
+                                          int(self.autoreset), self._eng.stream()))
+        return self._package(obs, ret, te, tr, tl, fobs, bufs)
+
+    def step_trajectory(self, des_pos, des_vel):
+        """BB step with caller-supplied desired trajectories [N, T, dof] f32 (no MP evaluation)."""
+        N, T, n = self.num_envs, self.T, self.dof
+        p = torch.as_tensor(des_pos, device=self.device).to(torch.float32).contiguous()
+        v = torch.as_tensor(des_vel, device=self.device).to(torch.float32).contiguous()
+        if tuple(p.shape) != (N, T, n) or tuple(v.shape) != (N, T, n):
+            raise ValueError(f"desired trajectories must be {(N, T, n)}")
+        obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
+        fobs = torch.empty_like(obs)
+        ret = torch.empty(N, dtype=torch.float64, device=self.device)
+        te = torch.empty(N, dtype=torch.uint8, device=self.device)
+        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        tl = torch.empty(N, dtype=torch.int32, device=self.device)
+        info_s, bufs = self._info_buffers()
+        _lib.check(self._eng.lib.fgx_step_traj(self._eng.h, _ptr(p), _ptr(v), _ptr(obs), _ptr(ret), _ptr(te),
+                                               _ptr(tr), _ptr(tl), _ptr(fobs),
+                                               ctypes.byref(info_s) if info_s is not None else None,
+                                               int(self.autoreset), self._eng.stream()))
+        if bufs:
+            bufs["positions"], bufs["velocities"] = p, v
+        return self._package(obs, ret, te, tr, tl, fobs, bufs)
+
+    def _package(self, obs, ret, te, tr, tl, fobs, bufs):
+        term, trunc = te.bool(), tr.bool()
+        if self.meta["reward_aggregation"] == "mean":
+            ret = ret / tl.to(torch.float64)
+        info = {"trajectory_length": tl}
+        if self.autoreset:
+            done = term | trunc
+            info["final_observation"] = fobs
+            info["_final_observation"] = done
+        else:
+            info["final_observation"] = fobs
+        info.update(bufs)
+        return obs, ret, term, trunc, info
+
+    def trajectory(self, actions):
+        """Desired (pos, vel) [N, T, dof] of the next plan (BlackBoxWrapper.get_trajectory)."""
+        a = self._check_actions(actions)
+        N, T, n = self.num_envs, self.T, self.dof
+        pos = torch.empty((N, T, n), dtype=torch.float32, device=self.device)
+        vel = torch.empty_like(pos)
+        _lib.check(self._eng.lib.fgx_trajectory(self._eng.h, _ptr(a), _ptr(pos), _ptr(vel), self._eng.stream()))
+        return pos, vel
+
+    # ------------------------------------------------------------------ fast path (bench)
+    def step_into(self, actions, obs, ret, te, tr, tl, fobs=None):
+        """Allocation-free BB step into preallocated buffers (no checks; for benchmarks)."""
+        self._eng.lib.fgx_step(self._eng.h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
+                               ctypes.c_void_p(ret.data_ptr()), ctypes.c_void_p(te.data_ptr()),
+                               ctypes.c_void_p(tr.data_ptr()), ctypes.c_void_p(tl.data_ptr()),
+                               ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, None,
+                               int(self.autoreset), self._eng.stream())
+
+    # ------------------------------------------------------------------ state / tables
+    def get_state(self):
+        N, n, dev = self.num_envs, self.dof, self.device
+        q = torch.empty((N, n), dtype=torch.float64, device=dev)
+        qd = torch.empty_like(q)
+        goal = torch.empty((N, 2), dtype=torch.float64, device=dev)
+        hole = torch.empty((N, 3), dtype=torch.float64, device=dev)
+        steps = torch.empty(N, dtype=torch.int32, device=dev)
+        _lib.check(self._eng.lib.fgx_get_state(self._eng.h, _ptr(q), _ptr(qd), _ptr(goal), _ptr(hole), _ptr(steps),
+                                               self._eng.stream()))
+        return dict(q=q, qd=qd, goal=goal, hole=hole, steps=steps)
+
+    def set_state(self, q=None, qd=None, goal=None, hole=None, steps=None):
+        def prep(x, dt):
+            return None if x is None else torch.as_tensor(x, device=self.device).to(dt).contiguous()
+        q, qd, goal, hole = (prep(x, torch.float64) for x in (q, qd, goal, hole))
+        steps = prep(steps, torch.int32)
+        _lib.check(self._eng.lib.fgx_set_state(self._eng.h, _ptr(q), _ptr(qd), _ptr(goal), _ptr(hole), _ptr(steps),
+                                               self._eng.stream()))
+
+    def tables(self):
+        d = self._eng.dims
+        out = torch.empty((d.table_rows, d.table_stride), dtype=torch.float32, device=self.device)
+        _lib.check(self._eng.lib.fgx_get_tables(self._eng.h, _ptr(out), self._eng.stream()))
+        return out
+
+    def close(self):
+        self._eng.close()
+
+
+class StepVectorEnv:
+    """N step-based reacher envs ('fancy/SimpleReacher-v0' ...), actions applied unclipped."""
+
+    def __init__(self, env_id, num_envs, device="cuda", autoreset=True, seed_offset=0, **env_kwargs):
+        cfg, meta = resolve(env_id, None, **env_kwargs)
+        if meta["mp_type"] is not None:
+            raise ValueError(f"{env_id} is a black-box id; use BlackBoxVectorEnv")
+        self.meta = meta
+        self.num_envs = int(num_envs)
+        self.autoreset = bool(autoreset)
+        self.seed_offset = int(seed_offset)
+        self._eng = _Engine(cfg, num_envs, device)
+        d = self._eng.dims
+        self.dof, self.obs_dim = d.dof, d.obs_dim
+        self.device = self._eng.device
+        bound = float(cfg.act_high)
+        self.single_action_space = Box(-bound, bound, (self.dof,), np.float32)
+
+    def reset(self, *, seed=None, options=None):
+        N = self.num_envs
+        obs = torch.empty((N, self.obs_dim), dtype=torch.float32, device=self.device)
+        seeds = None
+        if seed is not None:
+            seeds = (torch.arange(N, dtype=torch.int64, device=self.device) + (int(seed) + self.seed_offset)).contiguous()
+        _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), None, _ptr(obs), self._eng.stream()))
+        return obs, {}
+
+    def step(self, actions):
+        a = torch.as_tensor(actions, device=self.device).to(torch.float32).contiguous()
+        N = self.num_envs
+        if tuple(a.shape) != (N, self.dof):
+            raise ValueError(f"actions must have shape {(N, self.dof)}")
+        obs = torch.empty((N, self.obs_dim), dtype=torch.float32, device=self.device)
+        fobs = torch.empty_like(obs)
+        rew = torch.empty(N, dtype=torch.float64, device=self.device)
+        te = torch.empty(N, dtype=torch.uint8, device=self.device)
+        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        _lib.check(self._eng.lib.fgx_step_raw(self._eng.h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(te), _ptr(tr),
+                                              _ptr(fobs), int(self.autoreset), self._eng.stream()))
+        term, trunc = te.bool(), tr.bool()
+        info = {"final_observation": fobs, "_final_observation": term | trunc}
+        return obs, rew, term, trunc, info
+
+    def get_state(self):
+        return BlackBoxVectorEnv.get_state(self)
+
+    def close(self):
+        self._eng.close()
+
+
+def math_isnan(x):
+    return x != x

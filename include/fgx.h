@@ -1,0 +1,180 @@
+/*
+ * fgx.h — C ABI of libfgx.so, the MI355X (gfx950) black-box rollout engine.
+ *
+ * Drop-in boundary for the fancy_gym black-box reacher path.  The reference has no native
+ * code: each entry point below replaces a *Python* interface of the reference
+ * (paths relative to /root/reference/fancy_gym):
+ *
+ *   fgx_create        make_bb(...) / bb_env_constructor(...)            utils/make_env_helpers.py:68-136,
+ *                     (+ BlackBoxWrapper.__init__)                      envs/registry.py:280-309,
+ *                                                                       black_box/black_box_wrapper.py:17-88
+ *   fgx_reset         BlackBoxWrapper.reset -> env.reset(seed)          black_box/black_box_wrapper.py:258-267,
+ *                                                                       base_reacher/base_reacher.py:73-93,
+ *                                                                       simple_reacher/simple_reacher.py:46-54,
+ *                                                                       hole_reacher/hole_reacher.py:242-253
+ *   fgx_step          BlackBoxWrapper.step(action) (+ VectorEnv         black_box/black_box_wrapper.py:170-253
+ *                     autoreset)                                        (gymnasium SyncVectorEnv.step [EXT-M])
+ *   fgx_step_traj     BlackBoxWrapper.step with the desired trajectory  black_box/black_box_wrapper.py:177-253
+ *                     supplied by the caller (get_trajectory skipped)
+ *   fgx_trajectory    BlackBoxWrapper.get_trajectory(action)            black_box/black_box_wrapper.py:106-140
+ *                     -> MPInterface.get_traj_pos/get_traj_vel          (mp_pytorch, EXTERNAL)
+ *   fgx_step_raw      step-based env.step(action) (+ autoreset)         base_reacher/base_reacher_torque.py:20-37,
+ *                                                                       base_reacher/base_reacher_direct.py:20-38
+ *   fgx_get_state /   env.unwrapped.current_pos/current_vel, goal, hole black_box/raw_interface_wrapper.py:24-44
+ *   fgx_set_state     (checkpoint/test access)
+ *   fgx_get_tables    basis tables (test/introspection)
+ *
+ * Conventions
+ *   - Every array argument is a CALLER-OWNED DEVICE pointer (e.g. torch tensor storage) on the
+ *     handle's device, contiguous, row-major with the env index outermost ("[N, ...]").
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All work is
+ *     stream-ordered; no call synchronises the host except fgx_create / fgx_destroy.
+ *   - Return value: 0 on success, a negative FGX_E* code on error; fgx_last_error() returns a
+ *     thread-local message.  Nothing throws across the ABI.
+ *   - A handle is bound to one device; calls on one handle are not re-entrant.  Distinct
+ *     handles may be driven from distinct threads / processes (one per GPU).
+ *   - Floating point: env state is f64 (as the reference's numpy state), MP trajectories f32
+ *     (as mp_pytorch's torch f32), observations f32, rewards/returns f64.
+ */
+#ifndef FGX_H
+#define FGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FGX_ABI_VERSION 1
+
+/* error codes */
+#define FGX_OK 0
+#define FGX_E_INVALID (-1)   /* bad argument / configuration (reference: ValueError)         */
+#define FGX_E_HIP (-2)       /* HIP runtime error                                            */
+#define FGX_E_NOMEM (-3)     /* device allocation failed                                     */
+#define FGX_E_UNSUPPORTED (-4) /* configuration outside what the engine implements           */
+
+/* env kinds (reference: SimpleReacherEnv = torque, HoleReacherEnv = direct velocity) */
+#define FGX_ENV_SIMPLE 0
+#define FGX_ENV_HOLE 1
+
+/* trajectory generators (reference: trajectory_generator_factory.py:7-21) */
+#define FGX_MP_NONE 0   /* step-based env only (fgx_step_raw)                */
+#define FGX_MP_PROMP 1
+#define FGX_MP_DMP 2
+#define FGX_MP_PRODMP 3
+
+/* phase generators (phase_generator_factory.py:9-23) */
+#define FGX_PHASE_LINEAR 0
+#define FGX_PHASE_EXP 1
+
+/* tracking controllers (controller_factory.py:10-24) */
+#define FGX_CTRL_PD 0        /* "motor"    pd_controller.py:21-29  */
+#define FGX_CTRL_VEL 1       /* "velocity" vel_controller.py:8-9   */
+#define FGX_CTRL_POS 2       /* "position" pos_controller.py:8-9   */
+
+typedef struct fgx_config {
+  int32_t abi_version;          /* = FGX_ABI_VERSION                                        */
+  int32_t env_kind;             /* FGX_ENV_*                                                */
+  int32_t n_links;              /* 1..8                                                     */
+  int32_t random_start;         /* base_reacher.py:81-86                                    */
+  int32_t allow_self_collision; /* HoleReacher only                                         */
+  int32_t allow_wall_collision; /* HoleReacher only                                         */
+  int32_t mp_kind;              /* FGX_MP_*                                                 */
+  int32_t phase_kind;           /* FGX_PHASE_*                                              */
+  int32_t n_basis;              /* basis functions per dof (without zero padding)          */
+  int32_t zero_start;           /* ZeroPaddingNormalizedRBF num_basis_zero_start            */
+  int32_t zero_goal;            /* ZeroPaddingNormalizedRBF num_basis_zero_goal             */
+  int32_t ctrl_kind;            /* FGX_CTRL_*                                               */
+  int32_t T;                    /* samples per plan = round(duration/dt)                    */
+  int32_t max_episode_steps;    /* TimeLimit (registry max_episode_steps)                   */
+  int32_t replan_period;        /* 0 = none; else replanning_schedule: t % period == 0      */
+  int32_t max_planning_times;   /* <= 0 : unlimited                                         */
+  int32_t condition_on_desired; /* black_box_wrapper.py:235-237                             */
+  int32_t time_aware;           /* TimeAwareObservation appended (utils/wrappers.py:49-63)  */
+  int32_t return_context;       /* context-mask the BB observation (black_box_wrapper.py:90-95) */
+  int32_t reserved0;
+  double dt;                    /* env dt (base_reacher.py:21)                              */
+  double duration;              /* BB duration (make_env_helpers.py:110-111)                */
+  double tau, delay, alpha_phase; /* phase generator                                        */
+  double bandwidth;             /* basis_bandwidth_factor                                   */
+  double weights_scale, goal_scale;
+  double alpha;                 /* DMP / ProDMP spring constant                             */
+  double pc_length;             /* ProDMP pre_compute_length_factor                         */
+  double p_gain, d_gain;        /* PD gains                                                 */
+  double act_low, act_high;     /* env action-space bounds as stored by gymnasium Box (f32) */
+  double hole_width, hole_depth, hole_x; /* NaN = sampled at reset (hole_reacher.py:261-294) */
+  double collision_penalty;     /* HoleReacher reward (hr_simple_reward.py:14)              */
+} fgx_config;
+
+typedef struct fgx_dims {
+  int32_t n_envs, dof, obs_dim, ctx_dim, out_obs_dim, n_params, T, table_rows, table_stride;
+  int32_t reserved[7];
+} fgx_dims;
+
+/* Optional per-step outputs of fgx_step / fgx_step_traj (black_box_wrapper.py:185-249,
+ * verbose >= 2).  Any pointer may be NULL.  Steps after trajectory_length are left untouched. */
+typedef struct fgx_info {
+  float* positions;      /* [N, T, dof]  desired positions                                 */
+  float* velocities;     /* [N, T, dof]  desired velocities                                */
+  double* step_actions;  /* [N, T, dof]  clipped controller actions                        */
+  float* step_obs;       /* [N, T, obs_dim + time_aware]  full (unmasked) observations     */
+  double* step_rewards;  /* [N, T]                                                         */
+  uint8_t* is_collided;  /* [N, T]  HoleReacher info                                       */
+  uint8_t* is_success;   /* [N, T]  HoleReacher info                                       */
+  double* end_effector;  /* [N, T, 2] HoleReacher info                                     */
+  double* reward_dist;   /* [N, T]  SimpleReacher info                                     */
+  double* reward_ctrl;   /* [N, T]  SimpleReacher info                                     */
+} fgx_info;
+
+const char* fgx_last_error(void);
+int fgx_abi_version(void);
+
+int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle);
+int fgx_destroy(void* handle);
+int fgx_get_dims(void* handle, fgx_dims* out);
+
+/* Reset the envs where mask[i] != 0 (mask NULL = all).  seeds: device u64 [N] or NULL
+ * (NULL = continue each env's own PCG64 stream, i.e. reset() without a seed).
+ * obs_out: [N, out_obs_dim] f32; rows of envs not reset are left untouched. */
+int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, float* obs_out, void* stream);
+
+/* One black-box step for all N envs: MP parameters params [N, n_params] f32 ->
+ * obs [N, out_obs_dim] f32 (already auto-reset for finished envs), ret [N] f64 (episode-segment
+ * return, np.sum aggregation), terminated/truncated [N] u8, traj_len [N] i32,
+ * final_obs [N, out_obs_dim] f32 (observation before the auto-reset; may be NULL), info (NULL ok).
+ * autoreset != 0 resets envs whose terminated|truncated is set (gymnasium VectorEnv). */
+int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t* terminated,
+             uint8_t* truncated, int32_t* traj_len, float* final_obs, const fgx_info* info,
+             int32_t autoreset, void* stream);
+
+/* Same as fgx_step but with caller-supplied desired trajectories pos/vel [N, T, dof] f32. */
+int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, float* obs,
+                  double* ret, uint8_t* terminated, uint8_t* truncated, int32_t* traj_len,
+                  float* final_obs, const fgx_info* info, int32_t autoreset, void* stream);
+
+/* Desired trajectories for the next plan of every env (initial conditions = current state),
+ * pos/vel [N, T, dof] f32 — the MFMA basis x weights GEMM path. */
+int fgx_trajectory(void* handle, const float* params, float* des_pos, float* des_vel, void* stream);
+
+/* Step-based env.step for all N envs: actions [N, dof] f32 applied unclipped (as the raw
+ * reference env), obs [N, obs_dim] f32, reward [N] f64, terminated/truncated [N] u8,
+ * final_obs (NULL ok).  autoreset as in fgx_step. */
+int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward,
+                 uint8_t* terminated, uint8_t* truncated, float* final_obs, int32_t autoreset,
+                 void* stream);
+
+/* State access (tests / checkpoint): q, qd [N, dof] f64, goal [N, 2] f64, hole [N, 3] f64
+ * (x, width, depth), steps [N] i32.  Any pointer may be NULL. */
+int fgx_get_state(void* handle, double* q, double* qd, double* goal, double* hole, int32_t* steps,
+                  void* stream);
+int fgx_set_state(void* handle, const double* q, const double* qd, const double* goal,
+                  const double* hole, const int32_t* steps, void* stream);
+
+/* Copy the f32 basis tables [table_rows, table_stride] to out (device). */
+int fgx_get_tables(void* handle, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FGX_H */

@@ -212,7 +212,7 @@ class BatchedBB:
 
     def __init__(self, name, N, ctrl, mp_spec=None, traj_fn=None, replan_period=0,
                  max_planning_times=np.inf, condition_on_desired=False, info_level=0,
-                 time_aware=None):
+                 time_aware=None, tables=None):
         self.env = BatchedReacher(name, N)
         self.N = N
         self.ctrl = ctrl
@@ -225,7 +225,8 @@ class BatchedBB:
         self.info_level = info_level
         if traj_fn is None:
             self.T = mp_spec.T
-            self.tables = mpm.build_tables(mp_spec, MAX_EPISODE_STEPS + self.T + 2)
+            self.tables = tables if tables is not None else mpm.build_tables(
+                mp_spec, (MAX_EPISODE_STEPS if replan_period > 0 else 0) + self.T + 2)
             traj_fn = lambda params, s0, q, qd: mpm.trajectory(mp_spec, self.tables, params, s0, q, qd)
         self.traj_fn = traj_fn
         self.traj_steps = np.zeros(N, np.int64)

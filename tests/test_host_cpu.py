@@ -1,0 +1,132 @@
+"""CPU-only checks of the boundary and the host layer (no kernel is launched here).
+
+Re-expresses the reference's structural tests (test/test_black_box.py, test/test_fancy_registry.py)
+for the reacher path: id registration, config merge, action / context space sizes, error types.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import fancy_gym_crowd_amd as fgx
+from fancy_gym_crowd_amd import _lib, registry
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ensure_built():
+    if not os.path.exists(_lib.LIB_PATH):
+        from fancy_gym_crowd_amd import _build
+        _build.build()
+
+
+def test_library_exports_every_declared_symbol():
+    _ensure_built()
+    header = open(os.path.join(ROOT, "include", "fgx.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(fgx_\w+)\s*\(", header, re.M))
+    assert declared, "no declarations parsed"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = declared - exported
+    assert not missing, f"declared in include/fgx.h but not exported: {missing}"
+    assert declared == set(_lib.EXPORTS), "ctypes binding out of sync with include/fgx.h"
+
+
+def test_library_loads_and_reports_abi():
+    _ensure_built()
+    lib = _lib.load()
+    assert lib.fgx_abi_version() == _lib.FGX_ABI_VERSION
+    # argument validation happens before any device work
+    cfg = _lib.FgxConfig()
+    cfg.abi_version = 999
+    h = ctypes.c_void_p()
+    assert lib.fgx_create(ctypes.byref(cfg), 4, 0, ctypes.byref(h)) == -1
+    assert b"abi" in lib.fgx_last_error()
+
+
+def test_config_struct_layout_matches_header():
+    # 20 int32 then 18 doubles (see include/fgx.h)
+    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8
+    assert ctypes.sizeof(_lib.FgxInfo) == 10 * 8
+
+
+def test_registry_ids():
+    # registry.py:243 -> '{ns}_{mp}/{name}'
+    for mp in fgx.KNOWN_MPS:
+        for name in ("SimpleReacher-v0", "LongSimpleReacher-v0", "HoleReacher-v0"):
+            assert f"fancy_{mp}/{name}" in fgx.ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS[mp]
+    assert len(fgx.ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS["all"]) == 9
+    assert fgx.MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS["fancy"]["ProDMP"]
+
+
+def test_nested_update_type_key_replaces():
+    base = {"controller_kwargs": {"controller_type": "motor", "p_gains": 1.0, "d_gains": 0.1}}
+    out = fgx.nested_update(base, {"controller_kwargs": {"controller_type": "velocity"}})
+    assert out["controller_kwargs"] == {"controller_type": "velocity"}
+    out = fgx.nested_update({"a": {"b": 1, "c": 2}}, {"a": {"c": 3}})
+    assert out == {"a": {"b": 1, "c": 3}}
+
+
+@pytest.mark.parametrize("mp,name,n_params,ctrl,p,d", [
+    ("ProMP", "SimpleReacher-v0", 10, _lib.CTRL_PD, 0.6, 0.075),
+    ("ProMP", "LongSimpleReacher-v0", 25, _lib.CTRL_PD, 0.6, 0.075),
+    ("DMP", "LongSimpleReacher-v0", 30, _lib.CTRL_PD, 0.6, 0.075),
+    ("ProDMP", "SimpleReacher-v0", 12, _lib.CTRL_PD, 1.0, 0.1),
+    ("ProMP", "HoleReacher-v0", 25, _lib.CTRL_VEL, None, None),
+    ("DMP", "HoleReacher-v0", 30, _lib.CTRL_VEL, None, None),
+    ("ProDMP", "HoleReacher-v0", 30, _lib.CTRL_PD, 1.0, 0.1),
+])
+def test_resolved_configs(mp, name, n_params, ctrl, p, d):
+    c, meta = fgx.resolve(f"fancy_{mp}/{name}")
+    assert meta["n_params"] == n_params                         # test_black_box.py:168-193
+    assert c.ctrl_kind == ctrl
+    if p is not None:
+        assert (c.p_gain, c.d_gain) == (p, d)
+    assert c.T == 200 and c.duration == 2.0                     # make_env_helpers.py:110-113
+    assert c.tau == (1.5 if mp == "ProDMP" else 2.0)
+    if mp == "DMP":
+        assert c.weights_scale == (50 if "Simple" in name else 500)
+        assert c.alpha_phase == (2 if "Simple" in name else 2.5)
+    if mp == "ProMP":
+        assert c.zero_start == 1 and c.n_basis == 5
+        assert c.weights_scale == (2 if "Hole" in name else 1)
+    if "Hole" in name:
+        assert c.act_high == float(np.float32(2 * np.pi))       # Box(float32) bound
+        assert np.isnan(c.hole_width) and np.isnan(c.hole_x) and c.hole_depth == 1.0
+        assert c.collision_penalty == 100
+
+
+def test_replanning_schedule_compiles_to_period():
+    c, _ = fgx.resolve("fancy_ProDMP/SimpleReacher-v0",
+                       {"black_box_kwargs": {"replanning_schedule": lambda pos, vel, obs, action, t: t % 25 == 0}})
+    assert c.replan_period == 25 and c.time_aware == 1 and c.return_context == 0
+    with pytest.raises(NotImplementedError):
+        fgx.resolve("fancy_ProDMP/SimpleReacher-v0",
+                    {"black_box_kwargs": {"replanning_schedule": lambda pos, vel, obs, action, t: t in (3, 50)}})
+    with pytest.raises(NotImplementedError):
+        fgx.resolve("fancy_ProDMP/SimpleReacher-v0",
+                    {"black_box_kwargs": {"replanning_schedule": lambda pos, vel, obs, action, t: pos[0] > 0.5}})
+
+
+def test_errors_mirror_reference():
+    with pytest.raises(ValueError):   # unknown controller type (controller_factory.py:22-24)
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", {"controller_kwargs": {"controller_type": "foo"}})
+    with pytest.raises(ValueError):   # unknown trajectory generator (trajectory_generator_factory.py:19-21)
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", {"trajectory_generator_kwargs": {"trajectory_generator_type": "x"}})
+    with pytest.raises(ValueError):   # sub-trajectories + replanning (make_env_helpers.py:91-92)
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", {"black_box_kwargs": {
+            "learn_sub_trajectories": True, "replanning_schedule": lambda *a: False}})
+    with pytest.raises(ValueError):
+        fgx.resolve("fancy_XYZ/SimpleReacher-v0")
+
+
+def test_context_space_sizes():
+    # test_black_box.py:153-165: BB obs shape == context_mask.sum()
+    for name, ctx in (("SimpleReacher-v0", 8), ("LongSimpleReacher-v0", 17), ("HoleReacher-v0", 18)):
+        c, _ = fgx.resolve(f"fancy_ProMP/{name}")
+        n = c.n_links
+        full = 3 * n + 3 if "Simple" in name else 3 * n + 4
+        assert ctx == full - 1
