@@ -111,11 +111,12 @@ def main():
     te = torch.empty(N, dtype=torch.uint8, device=dev)
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     tl = torch.empty(N, dtype=torch.int32, device=dev)
-    acc = torch.zeros((), dtype=torch.int64, device=dev)
+    acc = torch.zeros(1, dtype=torch.int64, device=dev)   # device counter of inner env steps
 
     for _ in range(args.warmup):
         env.step_into(params, obs, ret, te, tr, tl, fobs)
     torch.cuda.synchronize()
+    acc.zero_()
 
     K = args.steps
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
@@ -126,9 +127,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(K):
         ev0[k].record()
-        env.step_into(params, obs, ret, te, tr, tl, fobs)
+        env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
         ev1[k].record()
-        acc += tl.sum()
     if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
         gathered = [torch.empty_like(ret) for _ in range(world)]
         dist.all_gather(gathered, ret)

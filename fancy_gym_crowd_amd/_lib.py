@@ -40,7 +40,7 @@ class FgxDims(ctypes.Structure):
 class FgxInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "positions", "velocities", "step_actions", "step_obs", "step_rewards", "is_collided",
-        "is_success", "end_effector", "reward_dist", "reward_ctrl")]
+        "is_success", "end_effector", "reward_dist", "reward_ctrl", "inner_steps")]
 
 
 EXPORTS = {
@@ -51,10 +51,10 @@ EXPORTS = {
     "fgx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fgx_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FgxDims)]),
     "fgx_reset": (ctypes.c_int, [ctypes.c_void_p] * 5),
-    "fgx_step": (ctypes.c_int, [ctypes.c_void_p] * 9 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
+    "fgx_step": (ctypes.c_int, [ctypes.c_void_p] * 8 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
                                                          ctypes.c_void_p]),
-    "fgx_step_traj": (ctypes.c_int, [ctypes.c_void_p] * 10 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
-                                                               ctypes.c_void_p]),
+    "fgx_step_traj": (ctypes.c_int, [ctypes.c_void_p] * 9 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
+                                                              ctypes.c_void_p]),
     "fgx_trajectory": (ctypes.c_int, [ctypes.c_void_p] * 5),
     "fgx_step_raw": (ctypes.c_int, [ctypes.c_void_p] * 7 + [ctypes.c_int32, ctypes.c_void_p]),
     "fgx_get_state": (ctypes.c_int, [ctypes.c_void_p] * 7),

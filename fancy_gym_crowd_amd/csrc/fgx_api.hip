@@ -12,7 +12,9 @@
 
 #include "../../include/fgx.h"
 #include "fgx_kernels.h"
+#include "fgx_tables.h"
 #include "fgx_aux.h"
+#include "fgx_dispatch.h"
 
 using namespace fgx;
 
@@ -46,59 +48,17 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 }  // namespace
 
-// ------------------------------------------------------------------------ dispatch tables
-// Instantiated shapes: n_links in {2, 5}, n_basis = 5 (every registered reacher MP config).
+// ------------------------------------------------------------------------ dispatch
+// The episode kernels are instantiated per env kind in their own translation units
+// (fgx_ep_simple.hip, fgx_ep_hole.hip) so that the build compiles them in parallel.
 #define FGX_FOR_NL(X) X(2) X(5)
-
-template <int ENV, int MP, int CTRL, int NL>
-static int launch_episode_nl(const Handle& h, const float* params, const float* dpos, const float* dvel,
-                             const Outputs& o, hipStream_t stream) {
-  const int threads = 256;
-  const int blocks = (int)((h.dc.N + threads - 1) / threads);
-  const size_t lds = (MP == MP_GIVEN) ? 0 : (size_t)h.dc.rows * h.dc.stride * sizeof(float);
-  hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, 5>), dim3(blocks), dim3(threads), lds, stream, h.dc, h.st,
-                     params, dpos, dvel, o);
-  HIP_TRY(hipGetLastError());
-  return FGX_OK;
-}
-
-template <int ENV, int MP, int CTRL>
-static int launch_episode_ctrl(const Handle& h, const float* params, const float* dpos, const float* dvel,
-                               const Outputs& o, hipStream_t stream) {
-#define X(NL) \
-  if (h.dc.nl == NL) return launch_episode_nl<ENV, MP, CTRL, NL>(h, params, dpos, dvel, o, stream);
-  FGX_FOR_NL(X)
-#undef X
-  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
-}
-
-template <int ENV, int MP>
-static int launch_episode_mp(const Handle& h, const float* params, const float* dpos, const float* dvel,
-                             const Outputs& o, hipStream_t stream) {
-  switch (h.dc.ctrl) {
-    case CTRL_PD: return launch_episode_ctrl<ENV, MP, CTRL_PD>(h, params, dpos, dvel, o, stream);
-    case CTRL_VEL: return launch_episode_ctrl<ENV, MP, CTRL_VEL>(h, params, dpos, dvel, o, stream);
-    case CTRL_POS: return launch_episode_ctrl<ENV, MP, CTRL_POS>(h, params, dpos, dvel, o, stream);
-  }
-  return fail(FGX_E_INVALID, "bad ctrl_kind");
-}
-
-template <int ENV>
-static int launch_episode_env(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
-                              const Outputs& o, hipStream_t stream) {
-  switch (mp) {
-    case MP_PROMP: return launch_episode_mp<ENV, MP_PROMP>(h, params, dpos, dvel, o, stream);
-    case MP_DMP: return launch_episode_mp<ENV, MP_DMP>(h, params, dpos, dvel, o, stream);
-    case MP_PRODMP: return launch_episode_mp<ENV, MP_PRODMP>(h, params, dpos, dvel, o, stream);
-    case MP_GIVEN: return launch_episode_mp<ENV, MP_GIVEN>(h, params, dpos, dvel, o, stream);
-  }
-  return fail(FGX_E_INVALID, "bad mp kind");
-}
 
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
-  if (h.dc.env == ENV_SIMPLE) return launch_episode_env<ENV_SIMPLE>(h, mp, params, dpos, dvel, o, stream);
-  return launch_episode_env<ENV_HOLE>(h, mp, params, dpos, dvel, o, stream);
+  const int rc = (h.dc.env == ENV_SIMPLE)
+                     ? fgx_launch_episode_simple(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err)
+                     : fgx_launch_episode_hole(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
+  return rc;
 }
 
 static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, float* obs, hipStream_t stream) {
@@ -176,7 +136,7 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   if (c.mp_kind == FGX_MP_PRODMP) {
     d.stride = 2 * (c.n_basis + 1) + 4;
   } else {
-    d.stride = c.n_basis + 1;
+    d.stride = (c.n_basis + 2 + 3) & ~3;   // [basis..., dt32 | sdt, rcp(dt32), pad] (16-B rows)
   }
   if (c.mp_kind == FGX_MP_NONE) { d.rows = 0; d.stride = 0; }
   d.rand_width = std::isnan(c.hole_width);
@@ -193,6 +153,7 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.act_hi32 = (float)c.act_high;
   d.dt32 = (float)c.dt;
   d.tau32 = (float)c.tau;
+  d.rcp_tau32 = 1.0f / d.tau32;
   d.hole_w0 = c.hole_width;
   d.hole_d0 = c.hole_depth;
   d.hole_x0 = c.hole_x;
@@ -334,6 +295,7 @@ static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, i
     o.end_effector = info->end_effector;
     o.reward_dist = info->reward_dist;
     o.reward_ctrl = info->reward_ctrl;
+    o.inner_steps = (long long*)info->inner_steps;
   }
   return o;
 }
@@ -368,7 +330,7 @@ int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, floa
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
   o.positions = nullptr;
-  o.velocities = nullptr;
+  o.velocities = nullptr;   // the caller already holds the desired trajectories
   return launch_episode(*h, MP_GIVEN, nullptr, des_pos, des_vel, o, (hipStream_t)stream);
 }
 

@@ -40,7 +40,7 @@ struct DevCfg {
   int n_split;      // numpy pairwise split point for a T-long return sum (0: none)
   int ctx_idx[kMaxObs + 1];
   double dt, tau, p_gain, d_gain, act_lo, act_hi;
-  float act_lo32, act_hi32, dt32, tau32;
+  float act_lo32, act_hi32, dt32, tau32, rcp_tau32;
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
   float ws32, gs32, alpha32, beta32;
   double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
@@ -78,6 +78,7 @@ struct Outputs {
   double* end_effector;
   double* reward_dist;
   double* reward_ctrl;
+  long long* inner_steps;
   int autoreset;
 };
 
@@ -86,6 +87,26 @@ __device__ __forceinline__ double np_max(double x, double lo) { return (x != x) 
 __device__ __forceinline__ double np_min(double x, double hi) { return (x != x) ? x : (x < hi ? x : hi); }
 __device__ __forceinline__ float np_maxf(float x, float lo) { return (x != x) ? x : (x > lo ? x : lo); }
 __device__ __forceinline__ float np_minf(float x, float hi) { return (x != x) ? x : (x < hi ? x : hi); }
+
+// np.clip(x, lo, hi) = minimum(maximum(x, lo), hi) with NaN propagation (umath clip)
+__device__ __forceinline__ double np_clip(double x, double lo, double hi) {
+  const double y = __builtin_fmin(__builtin_fmax(x, lo), hi);
+  return (x != x) ? x : y;
+}
+__device__ __forceinline__ float np_clipf(float x, float lo, float hi) {
+  const float y = __builtin_fminf(__builtin_fmaxf(x, lo), hi);
+  return (x != x) ? x : y;
+}
+
+// Correctly rounded f32 x / d given r = RN(1/d) (Markstein: q = RN(x r), e = x - q d exact by
+// fma, RN(q + e r) == RN(x / d)); three instructions instead of the IEEE division sequence.
+// Exactness for the divisors the engine uses (the dt32 / tau32 table values) is checked by
+// tests/test_mp_structure.py::test_division_by_reciprocal_is_exact.
+__device__ __forceinline__ float div_rcp(float x, float d, float r) {
+  const float q = x * r;
+  const float e = __builtin_fmaf(-q, d, x);
+  return __builtin_fmaf(e, r, q);
+}
 
 // np.linalg.norm of a 2-vector == sqrt(ddot) == sqrt(fma(y, y, x*x)) (OpenBLAS order)
 __device__ __forceinline__ double norm2(double x, double y) { return __builtin_sqrt(__builtin_fma(y, y, x * x)); }
@@ -117,12 +138,23 @@ struct PairwiseSum {
     if (j == 7) tail = comb(r);
     else tail = tail + v;
   }
+  // compile-time slot J == k & 7 (the caller unrolls its loop by 8)
+  template <int J>
+  __device__ __forceinline__ static void push_ct(double* r, double& tail, bool first_block, double v) {
+    r[J] = first_block ? v : r[J] + v;
+    if (J == 7) tail = comb(r);
+    else tail = tail + v;
+  }
+  template <int J>
+  __device__ __forceinline__ void add_ct(int k, double v, int split) {
+    if (split > 0 && k == split) first = comb(a);
+    if (k < 128) push_ct<J>(a, t, k < 8, v);
+    if (split > 0 && k >= split) push_ct<J>(b, u, k - split < 8, v);
+  }
   __device__ __forceinline__ void add(int k, double v, int split) {
+    if (split > 0 && k == split) first = comb(a);   // blocks [0, split) only
     if (k < 128) push(a, t, k, v);
-    if (split > 0 && k >= split) {
-      if (k == split) first = comb(a);
-      push(b, u, k - split, v);
-    }
+    if (split > 0 && k >= split) push(b, u, k - split, v);
   }
   __device__ __forceinline__ double result(int L, int split) const {
     if (L <= 128 || split == 0) return t;

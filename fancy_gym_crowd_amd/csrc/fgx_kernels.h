@@ -12,150 +12,42 @@
 //   k_traj_valu   desired trajectories [N, T, dof] (reference path for k_traj_mfma)
 //   k_traj_mfma   desired trajectories as an f32 MFMA GEMM (v_mfma_f32_32x32x2_f32)
 #pragma once
+#include <type_traits>
+
 #include "fgx_device.h"
 
 namespace fgx {
 
-// ============================================================================ tables
-__device__ inline double phase64(const DevCfg& c, double t, double tau, double delay, double alpha_x) {
-  double lin = (t - delay) / tau;
-  lin = lin > 0.0 ? lin : 0.0;   // np.maximum(x, 0.0)
-  if (c.phase == 0) return lin < 1.0 ? lin : 1.0;
-  return exp((-alpha_x) * lin);
-}
-
-// normalized RBF at phase x, f64, all n = nb + zs + zg columns (oracle/mp.py:rbf64)
-__device__ inline void rbf64(const DevCfg& c, double alpha_x, double bw, double x, double* phi) {
-  const int n = c.nb + c.zs + c.zg;
-  double cen[kMaxBasis + 4], e[kMaxBasis + 4];
-  for (int j = 0; j < n; ++j) {
-    const double u = (n > 1) ? (double)j / (double)(n - 1) : 0.0;
-    cen[j] = (c.phase == 0) ? u : exp((-alpha_x) * u);
-  }
-  for (int j = 0; j < n; ++j) {
-    double d = (n > 1) ? ((j < n - 1) ? cen[j + 1] - cen[j] : cen[n - 1] - cen[n - 2]) : 1.0;
-    const double h = bw / (d * d);
-    const double dd = x - cen[j];
-    e[j] = exp((-h) * (dd * dd) / 2);
-  }
-  double s;
-  if (n < 8) {
-    s = e[0] + 0.0;
-    for (int j = 1; j < n; ++j) s = s + e[j];
-  } else {   // numpy pairwise (8 accumulators, n <= 128)
-    double r[8];
-    for (int j = 0; j < 8; ++j) r[j] = e[j];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8)
-      for (int j = 0; j < 8; ++j) r[j] = r[j] + e[i + j];
-    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) s = s + e[i];
-  }
-  for (int j = 0; j < n; ++j) phi[j] = e[j] / s;
-}
-
-// ProMP / DMP tables: one thread per row.
-__global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x, double bw, float* tab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.rows) return;
-  double phi[kMaxBasis + 4];
-  const double t = (double)i * c.dt;
-  const double x = phase64(c, t, tau, delay, alpha_x);
-  rbf64(c, alpha_x, bw, x, phi);
-  float* row = tab + (size_t)i * c.stride;
-  if (c.mp == MP_PROMP) {
-    for (int j = 0; j < c.nb; ++j) row[j] = (float)(c.weights_scale * phi[c.zs + j]);
-    const float t0 = (float)t, t1 = (float)((double)(i + 1) * c.dt);
-    row[c.nb] = t1 - t0;
-  } else {   // DMP: psi = x * phi ; sdt = f32(s_{i+1}) - f32(s_i)
-    for (int j = 0; j < c.nb; ++j) row[j] = (float)(x * phi[c.zs + j]);
-    double s0 = (t - delay) / tau, s1 = ((double)(i + 1) * c.dt - delay) / tau;
-    s0 = s0 > 0.0 ? s0 : 0.0;
-    s1 = s1 > 0.0 ? s1 : 0.0;
-    row[c.nb] = (float)s1 - (float)s0;
-  }
-}
-
-// ProDMP precompute (oracle/mp.py:prodmp_fine64).  Single block; scratch: [rows][2*nb] f64.
-__global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw, double* dp, float* tab) {
-  const int nb = c.nb, R = c.rows, W = 2 * nb;
-  const double h = c.dt / tau, a = c.alpha;
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {
-    const double s = (double)i * h;
-    const double x = exp((-alpha_x) * s);
-    double phi[kMaxBasis + 4];
-    rbf64(c, alpha_x, bw, x, phi);
-    const double e = exp(a * s / 2);
-    const double k1 = s * e * x, k2 = e * x;
-    for (int j = 0; j < nb; ++j) {
-      dp[(size_t)i * W + j] = k1 * phi[c.zs + j];
-      dp[(size_t)i * W + nb + j] = k2 * phi[c.zs + j];
-    }
-  }
-  __syncthreads();
-  // cumulative trapezoid, one thread per column, sequential (same order as the oracle)
-  if ((int)threadIdx.x < W) {
-    const int j = threadIdx.x;
-    double p = 0.0, prev = dp[j];
-    dp[j] = 0.0;
-    for (int i = 1; i < R; ++i) {
-      const double cur = dp[(size_t)i * W + j];
-      p = p + h * (prev + cur) / 2;
-      dp[(size_t)i * W + j] = p;
-      prev = cur;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {
-    const double s = (double)i * h;
-    const double e = exp(a * s / 2);
-    const double y1 = exp((-a) * s / 2);
-    const double y2 = s * y1;
-    const double dy1 = -a / 2 * y1;
-    const double dy2 = -a / 2 * y2 + y1;
-    const double q1 = (a * s / 2 - 1) * e + 1;
-    const double q2 = a / 2 * (e - 1);
-    float* row = tab + (size_t)i * c.stride;
-    for (int j = 0; j < nb; ++j) {
-      const double p1 = dp[(size_t)i * W + j], p2 = dp[(size_t)i * W + nb + j];
-      row[j] = (float)(p2 * y2 - p1 * y1);
-      row[nb + 1 + j] = (float)(p2 * dy2 - p1 * dy1);
-    }
-    row[nb] = (float)(q2 * y2 - q1 * y1);
-    row[2 * nb + 1] = (float)(q2 * dy2 - q1 * dy1);
-    row[2 * nb + 2] = (float)y1;
-    row[2 * nb + 3] = (float)y2;
-    row[2 * nb + 4] = (float)dy1;
-    row[2 * nb + 5] = (float)dy2;
-  }
-}
-
 // ============================================================================ obs
-// Full env observation (simple_reacher.py:75-83 / hole_reacher.py:296-306) [+ t/max_steps]
+// Env observation (simple_reacher.py:75-83 / hole_reacher.py:296-306) [+ t/max_steps,
+// utils/wrappers.py:58-59], context-masked when `ctx` (black_box_wrapper.py:90-95), written
+// straight to up to two destinations (no private arrays: nothing spills to scratch).
 template <int NL>
-__device__ __forceinline__ void full_obs(const DevCfg& c, const Env<NL>& v, float* o) {
+__device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2) {
+  const bool rs = !ctx || c.random_start;
   int p = 0;
-  double sn[NL], cs[NL];
+  auto put = [&](float x) {
+    if (d1) d1[p] = x;
+    if (d2) d2[p] = x;
+    ++p;
+  };
+  if (rs) {
+    double sn[NL], cs[NL];
 #pragma unroll
-  for (int k = 0; k < NL; ++k) sincos(v.q[k], &sn[k], &cs[k]);
+    for (int k = 0; k < NL; ++k) sincos(v.q[k], &sn[k], &cs[k]);
 #pragma unroll
-  for (int k = 0; k < NL; ++k) o[p++] = (float)cs[k];
+    for (int k = 0; k < NL; ++k) put((float)cs[k]);
 #pragma unroll
-  for (int k = 0; k < NL; ++k) o[p++] = (float)sn[k];
+    for (int k = 0; k < NL; ++k) put((float)sn[k]);
 #pragma unroll
-  for (int k = 0; k < NL; ++k) o[p++] = (float)v.qd[k];
-  if (c.env == ENV_HOLE) o[p++] = (float)v.hw;
-  o[p++] = (float)(v.jx[NL] - v.gx);
-  o[p++] = (float)(v.jy[NL] - v.gy);
-  o[p++] = (float)v.steps;
-  if (c.time_aware) o[p++] = (float)((double)v.steps / (double)c.max_steps);
-}
-
-__device__ __forceinline__ void write_out_obs(const DevCfg& c, const float* full, float* dst) {
-  if (c.return_context) {
-    for (int j = 0; j < c.out_dim; ++j) dst[j] = full[c.ctx_idx[j]];
-  } else {
-    for (int j = 0; j < c.out_dim; ++j) dst[j] = full[j];
+    for (int k = 0; k < NL; ++k) put((float)v.qd[k]);
+  }
+  if (c.env == ENV_HOLE && (!ctx || c.rand_width)) put((float)v.hw);
+  put((float)(v.jx[NL] - v.gx));
+  put((float)(v.jy[NL] - v.gy));
+  if (!ctx) {
+    put((float)v.steps);
+    if (c.time_aware) put((float)((double)v.steps / (double)c.max_steps));
   }
 }
 
@@ -196,11 +88,7 @@ __global__ __launch_bounds__(256) void k_reset(DevCfg c, DevState s, const uint6
   store_env(c, s, e, v);
   s.plans[e] = 0;
   s.flags[e] = 0;
-  if (obs) {
-    float full[kMaxObs + 1];
-    full_obs(c, v, full);
-    write_out_obs(c, full, obs + e * c.out_dim);
-  }
+  if (obs) emit_obs(c, v, c.return_context, obs + e * c.out_dim, nullptr);
 }
 
 // ============================================================================ trajectories
@@ -273,12 +161,12 @@ struct Traj {
     if (MP == MP_PROMP) {
       if (k < T - 1) {
         const float* nrow = row + stride;
-        const float dti = row[NB];
+        const float dti = row[NB], rdt = row[NB + 1];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
           const float nx = chain(nrow, w[d]);
           pos[d] = cur[d];
-          vel[d] = (nx - cur[d]) / dti;
+          vel[d] = div_rcp(nx - cur[d], dti, rdt);
           cur[d] = nx;
           vprev[d] = vel[d];
         }
@@ -291,7 +179,7 @@ struct Traj {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         pos[d] = y[d];
-        vel[d] = z[d] / c.tau32;
+        vel[d] = div_rcp(z[d], c.tau32, c.rcp_tau32);
         if (k < T - 1) {
           const float f = chain(row, w[d]);
           const float acc = c.alpha32 * (c.beta32 * (g[d] - y[d]) - z[d]) + f;
@@ -308,14 +196,97 @@ struct Traj {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         pos[d] = chain(hp, w[d]);
-        vel[d] = chain(hv, w[d]) / c.tau32;
+        vel[d] = div_rcp(chain(hv, w[d]), c.tau32, c.rcp_tau32);
       }
     }
   }
 };
 
+// ============================================================================ env substep
+// One env.step with the (clipped) action a (f64) / a32 (when the action array is float32).
+// base_reacher_torque.py:20-37, base_reacher_direct.py:20-38, simple_reacher.py:56-70,
+// hole_reacher.py:255-259, hr_simple_reward.py:19-53.  Returns the reward; FK is refreshed
+// for HoleReacher always and for SimpleReacher only when the reward needs it or `fk_always`.
+struct StepOut {
+  double reward, rdist, rctrl;
+  bool coll, success;
+};
+
+template <int ENV, bool F32, int NL>
+__device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const double* a, const float* a32,
+                                           bool fk_always) {
+  StepOut r;
+  r.coll = false;
+  r.success = false;
+  r.rdist = 0.0;
+  const int st = v.steps;
+  if (ENV == ENV_SIMPLE) {
+#pragma unroll
+    for (int d = 0; d < NL; ++d) {
+      const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * a[d];
+      v.qd[d] = v.qd[d] + inc;
+      v.q[d] = v.q[d] + c.dt * v.qd[d];
+    }
+    double ctrl;
+    if (F32) {
+      float s32 = a32[0] * a32[0];
+#pragma unroll
+      for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
+      ctrl = (double)s32;
+    } else {
+      ctrl = a[0] * a[0];
+#pragma unroll
+      for (int d = 1; d < NL; ++d) ctrl = ctrl + a[d] * a[d];
+    }
+    if (st >= 199 || fk_always) v.fk();
+    if (st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+    r.reward = r.rdist - ctrl;
+    r.rctrl = ctrl;
+  } else {
+    double acc_cost;
+    if (F32 && (v.flags & 1u)) {   // qd already holds a float32 array: f32 arithmetic
+      float s32 = 0.0f;
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const float ac = (a32[d] - (float)v.qd[d]) / c.dt32;
+        s32 = (d == 0) ? ac * ac : s32 + ac * ac;
+      }
+      acc_cost = (double)s32;
+    } else {
+      acc_cost = 0.0;
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double ac = (a[d] - v.qd[d]) / c.dt;
+        acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < NL; ++d) {
+      v.qd[d] = a[d];
+      const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * v.qd[d];
+      v.q[d] = v.q[d] + inc;
+    }
+    if (F32) v.flags |= 1u;
+    v.fk();
+    const bool sc = c.allow_self ? false : v.self_collision();
+    const bool wc = c.allow_wall ? false : v.wall_collision(c);
+    r.coll = sc || wc;
+    if (st == 199 || r.coll) {
+      const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+      const double dc = dist * dist;
+      // np.dot([dist^2, acc, coll], [-1, -5e-8, -penalty]) == OpenBLAS forward fma chain
+      r.reward = __builtin_fma(r.coll ? 1.0 : 0.0, -c.penalty, __builtin_fma(acc_cost, -5e-8, dc * -1.0));
+      r.success = dist < 0.005 && !r.coll;
+    } else {
+      r.reward = acc_cost * -5e-8;
+    }
+  }
+  v.steps = st + 1;
+  return r;
+}
+
 // ============================================================================ the BB step
-template <int ENV, int MP, int CTRL, int NL, int NB>
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
 __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const float* __restrict__ params,
                                                  const float* __restrict__ dpos, const float* __restrict__ dvel,
                                                  Outputs o) {
@@ -349,12 +320,15 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   PairwiseSum ps;
   ps.init();
   const int split = c.n_split;
-  bool term = false, trunc = false;
-  int k = 0;
+  bool term = false, trunc = false, stop = false;
   float pos[NL], vel[NL];
-  const bool log = o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.reward_dist ||
-                   o.positions || o.end_effector;
-  for (k = 0; k < c.T; ++k) {
+  constexpr bool F32 = (CTRL != CTRL_PD);
+
+  // One plan sample k: desired state -> controller -> clip -> env.step -> return / info.
+  // J = k & 7 when known at compile time (unrolled fast loop), -1 otherwise.  Returns true
+  // when the BB step ends after this sample (black_box_wrapper.py:233-239).
+  auto sample = [&](int k, auto Jtag, bool fk_always) -> bool {
+    constexpr int J = decltype(Jtag)::value;
     if (MP == MP_GIVEN) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
@@ -367,108 +341,39 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // ---- tracking controller + clip (black_box_wrapper.py:201-205)
     double a[NL];
     float a32[NL];
-    constexpr bool F32 = (CTRL != CTRL_PD);
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       if (CTRL == CTRL_PD) {
         const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
-        a[d] = np_min(np_max(u, c.act_lo), c.act_hi);
+        a[d] = np_clip(u, c.act_lo, c.act_hi);
+        a32[d] = 0.0f;
       } else {
         const float u = (CTRL == CTRL_VEL) ? vel[d] : pos[d];
-        a32[d] = np_minf(np_maxf(u, c.act_lo32), c.act_hi32);
+        a32[d] = np_clipf(u, c.act_lo32, c.act_hi32);
         a[d] = (double)a32[d];
       }
     }
-    // ---- env.step (base_reacher_torque.py:20-37 / base_reacher_direct.py:20-38)
-    const int st = v.steps;
-    double reward;
-    bool coll = false, success = false;
-    double rdist = 0.0, rctrl = 0.0;
-    if (ENV == ENV_SIMPLE) {
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * a[d];
-        v.qd[d] = v.qd[d] + inc;
-        v.q[d] = v.q[d] + c.dt * v.qd[d];
-      }
-      double ctrl;
-      if (F32) {
-        float s32 = a32[0] * a32[0];
-#pragma unroll
-        for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
-        ctrl = (double)s32;
-      } else {
-        ctrl = a[0] * a[0];
-#pragma unroll
-        for (int d = 1; d < NL; ++d) ctrl = ctrl + a[d] * a[d];
-      }
-      double dist = 0.0;
-      if (st >= 199 || log) v.fk();
-      if (st >= 199) dist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
-      reward = dist - ctrl;
-      rdist = dist;
-      rctrl = ctrl;
-    } else {
-      double acc_cost;
-      if (F32 && (v.flags & 1u)) {
-        float s32 = 0.0f;
-#pragma unroll
-        for (int d = 0; d < NL; ++d) {
-          const float ac = (a32[d] - (float)v.qd[d]) / c.dt32;
-          s32 = (d == 0) ? ac * ac : s32 + ac * ac;
-        }
-        acc_cost = (double)s32;
-      } else {
-        acc_cost = 0.0;
-#pragma unroll
-        for (int d = 0; d < NL; ++d) {
-          const double ac = (a[d] - v.qd[d]) / c.dt;
-          acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
-        }
-      }
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        v.qd[d] = a[d];
-        const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * v.qd[d];
-        v.q[d] = v.q[d] + inc;
-      }
-      if (F32) v.flags |= 1u;
-      v.fk();
-      const bool sc = c.allow_self ? false : v.self_collision();
-      const bool wc = c.allow_wall ? false : v.wall_collision(c);
-      coll = sc || wc;
-      if (st == 199 || coll) {
-        const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
-        const double dc = dist * dist;
-        reward = __builtin_fma(coll ? 1.0 : 0.0, -c.penalty, __builtin_fma(acc_cost, -5e-8, dc * -1.0));
-        success = dist < 0.005 && !coll;
-      } else {
-        reward = acc_cost * -5e-8;
-      }
-    }
-    v.steps = st + 1;
-    term = (ENV == ENV_HOLE) ? coll : false;
+    // ---- env.step
+    const StepOut r = substep<ENV, F32, NL>(c, v, a, a32, fk_always);
+    term = (ENV == ENV_HOLE) ? r.coll : false;
     trunc = v.steps >= c.max_steps;
-    ps.add(k, reward, split);
-    // ---- info (verbose >= 2)
-    if (log) {
+    if constexpr (J >= 0) ps.template add_ct<J>(k, r.reward, split);
+    else ps.add(k, r.reward, split);
+    // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
+    if (LOG) {
       const int64_t ek = e * c.T + k;
       if (o.step_actions)
         for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = a[d];
       if (o.positions && MP != MP_GIVEN)
         for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
-      if (o.step_rewards) o.step_rewards[ek] = reward;
-      if (o.step_obs) {
-        float full[kMaxObs + 1];
-        full_obs(c, v, full);
-        for (int j = 0; j < c.full_dim; ++j) o.step_obs[ek * c.full_dim + j] = full[j];
-      }
+      if (o.step_rewards) o.step_rewards[ek] = r.reward;
+      if (o.step_obs) emit_obs(c, v, false, o.step_obs + ek * c.full_dim, nullptr);
       if (ENV == ENV_HOLE) {
-        if (o.is_collided) { o.is_collided[ek] = coll; o.is_success[ek] = success; }
+        if (o.is_collided) { o.is_collided[ek] = r.coll; o.is_success[ek] = r.success; }
         if (o.end_effector) { o.end_effector[ek * 2] = v.jx[NL]; o.end_effector[ek * 2 + 1] = v.jy[NL]; }
       } else if (o.reward_dist) {
-        o.reward_dist[ek] = rdist;
-        o.reward_ctrl[ek] = rctrl;
+        o.reward_dist[ek] = r.rdist;
+        o.reward_ctrl[ek] = r.rctrl;
       }
     }
     const bool replan_now = c.replan > 0 && ((k + 1 + s0) % c.replan == 0) &&
@@ -479,35 +384,65 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         for (int d = 0; d < NL; ++d) { s.cond[d * N + e] = pos[d]; s.cond[(NL + d) * N + e] = vel[d]; }
         v.flags |= 2u;
       }
-      break;
+      return true;
+    }
+    return false;
+  };
+
+  int k = 0;
+  if (!LOG) {
+    // fast path: blocks of 8 samples with compile-time return slots; SimpleReacher blocks
+    // never reach env step 199 (the only step whose reward needs FK)
+    while (!stop && k + 8 <= c.T && !(ENV == ENV_SIMPLE && v.steps + 8 > 199)) {
+#define FGX_SAMPLE(J) \
+      if (!stop) { stop = sample(k, std::integral_constant<int, J>{}, false); ++k; }
+      FGX_SAMPLE(0) FGX_SAMPLE(1) FGX_SAMPLE(2) FGX_SAMPLE(3)
+      FGX_SAMPLE(4) FGX_SAMPLE(5) FGX_SAMPLE(6) FGX_SAMPLE(7)
+#undef FGX_SAMPLE
     }
   }
+  while (!stop && k < c.T) {
+    stop = sample(k, std::integral_constant<int, -1>{}, LOG);
+    ++k;
+  }
+  k -= 1;   // index of the last executed sample
   const int L = (k < c.T) ? k + 1 : c.T;
-  // fill the remaining desired rows for info['positions'] (full plan is reported)
-  if (o.positions && MP != MP_GIVEN) {
+  // the full desired plan is reported (black_box_wrapper.py:245-246)
+  if (LOG && o.positions && MP != MP_GIVEN) {
     for (int kk = L; kk < c.T; ++kk) {
       tg.at(c, kk, pos, vel);
       const int64_t ek = e * c.T + kk;
       for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
     }
   }
-  if (ENV == ENV_SIMPLE && !log) v.fk();
-  float full[kMaxObs + 1];
-  full_obs(c, v, full);
+  if (ENV == ENV_SIMPLE && !LOG) v.fk();
   o.ret[e] = ps.result(L, split);
   o.term[e] = term;
   o.trunc[e] = trunc;
   o.tlen[e] = L;
-  if (o.final_obs) write_out_obs(c, full, o.final_obs + e * c.out_dim);
+  if (o.inner_steps) {   // wave-reduce the trajectory lengths, one atomic per (full) wave
+    if (__ballot(1) == ~0ull) {
+      long long sum = L;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+      if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
+    } else {
+      atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)L);
+    }
+  }
+  float* ob = o.obs + e * c.out_dim;
+  float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
   if (o.autoreset && (term || trunc)) {
-    Pcg64 r = load_rng(s.rng, N, e);
-    v.reset(c, r, false, 0);
-    store_rng(s.rng, N, e, r);
+    if (fo) emit_obs(c, v, c.return_context, fo, nullptr);
+    Pcg64 rg = load_rng(s.rng, N, e);
+    v.reset(c, rg, false, 0);
+    store_rng(s.rng, N, e, rg);
     plans = 0;
     v.flags = 0;
-    full_obs(c, v, full);
+    emit_obs(c, v, c.return_context, ob, nullptr);
+  } else {
+    emit_obs(c, v, c.return_context, ob, fo);
   }
-  write_out_obs(c, full, o.obs + e * c.out_dim);
   store_env(c, s, e, v);
   s.plans[e] = plans;
 }
@@ -523,72 +458,26 @@ __global__ __launch_bounds__(256) void k_step_raw(DevCfg c, DevState s, const fl
   Env<NL> v;
   load_env(c, s, e, v);
   float a32[NL];
+  double a[NL];
 #pragma unroll
-  for (int d = 0; d < NL; ++d) a32[d] = act[e * NL + d];
-  const int st = v.steps;
-  double reward;
-  bool coll = false;
-  if (ENV == ENV_SIMPLE) {
-#pragma unroll
-    for (int d = 0; d < NL; ++d) {
-      v.qd[d] = v.qd[d] + (double)(c.dt32 * a32[d]);
-      v.q[d] = v.q[d] + c.dt * v.qd[d];
-    }
-    float s32 = a32[0] * a32[0];
-#pragma unroll
-    for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
-    v.fk();
-    const double ctrl = (double)s32;
-    reward = (st >= 199) ? -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy) - ctrl : -ctrl;
-  } else {
-    double acc_cost;
-    if (v.flags & 1u) {
-      float s32 = 0.0f;
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const float ac = (a32[d] - (float)v.qd[d]) / c.dt32;
-        s32 = (d == 0) ? ac * ac : s32 + ac * ac;
-      }
-      acc_cost = (double)s32;
-    } else {
-      acc_cost = 0.0;
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double ac = ((double)a32[d] - v.qd[d]) / c.dt;
-        acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < NL; ++d) {
-      v.qd[d] = (double)a32[d];
-      v.q[d] = v.q[d] + (double)(c.dt32 * a32[d]);
-    }
-    v.flags |= 1u;
-    v.fk();
-    coll = (c.allow_self ? false : v.self_collision()) || (c.allow_wall ? false : v.wall_collision(c));
-    if (st == 199 || coll) {
-      const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
-      reward = __builtin_fma(coll ? 1.0 : 0.0, -c.penalty, __builtin_fma(acc_cost, -5e-8, dist * dist * -1.0));
-    } else {
-      reward = acc_cost * -5e-8;
-    }
-  }
-  v.steps = st + 1;
-  const bool te = (ENV == ENV_HOLE) && coll, tr = v.steps >= c.max_steps;
-  float full[kMaxObs + 1];
-  full_obs(c, v, full);
-  rew[e] = reward;
+  for (int d = 0; d < NL; ++d) { a32[d] = act[e * NL + d]; a[d] = (double)a32[d]; }
+  const StepOut r = substep<ENV, true, NL>(c, v, a, a32, true);
+  const bool te = (ENV == ENV_HOLE) && r.coll, tr = v.steps >= c.max_steps;
+  rew[e] = r.reward;
   term[e] = te;
   trunc[e] = tr;
-  if (final_obs) for (int j = 0; j < c.obs_dim; ++j) final_obs[e * c.obs_dim + j] = full[j];
+  float* ob = obs + e * c.obs_dim;
+  float* fo = final_obs ? final_obs + e * c.obs_dim : nullptr;
   if (autoreset && (te || tr)) {
-    Pcg64 r = load_rng(s.rng, N, e);
-    v.reset(c, r, false, 0);
-    store_rng(s.rng, N, e, r);
+    if (fo) emit_obs(c, v, false, fo, nullptr);
+    Pcg64 rg = load_rng(s.rng, N, e);
+    v.reset(c, rg, false, 0);
+    store_rng(s.rng, N, e, rg);
     v.flags = 0;
-    full_obs(c, v, full);
+    emit_obs(c, v, false, ob, nullptr);
+  } else {
+    emit_obs(c, v, false, ob, fo);
   }
-  for (int j = 0; j < c.obs_dim; ++j) obs[e * c.obs_dim + j] = full[j];
   store_env(c, s, e, v);
 }
 

@@ -125,10 +125,10 @@ __global__ __launch_bounds__(256) void k_traj_mfma(DevCfg c, DevState s, const f
             float vel;
             if (MP == MP_PROMP) {
               const int kc = k < T ? k : T - 1;
-              if (kc < T - 1) vel = (Q - P) / tab[(size_t)(kc + 1) * stride + NB];
-              else vel = (P - Q) / tab[(size_t)kc * stride + NB];
+              const float* dr = tab + (size_t)((kc < T - 1) ? kc + 1 : kc) * stride + NB;
+              vel = (kc < T - 1) ? div_rcp(Q - P, dr[0], dr[1]) : div_rcp(P - Q, dr[0], dr[1]);
             } else {
-              vel = Q / c.tau32;
+              vel = div_rcp(Q, c.tau32, c.rcp_tau32);
             }
             pv[r4 * NL + d] = P;
             vv[r4 * NL + d] = vel;

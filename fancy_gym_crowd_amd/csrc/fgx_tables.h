@@ -1,0 +1,126 @@
+// fgx_tables.h — basis-table kernels (included by fgx_api.hip only).
+//   k_tables_rbf     ProMP / DMP rows: normalized-RBF basis on the phase of t_i = i*dt
+//   k_tables_prodmp  ProDMP precompute: cumulative-trapezoid integrals + homogeneous solutions
+// All values are computed in f64 and rounded once to f32 (oracle/mp.py:build_tables).
+#pragma once
+#include "fgx_device.h"
+
+namespace fgx {
+
+// ============================================================================ tables
+__device__ inline double phase64(const DevCfg& c, double t, double tau, double delay, double alpha_x) {
+  double lin = (t - delay) / tau;
+  lin = lin > 0.0 ? lin : 0.0;   // np.maximum(x, 0.0)
+  if (c.phase == 0) return lin < 1.0 ? lin : 1.0;
+  return exp((-alpha_x) * lin);
+}
+
+// normalized RBF at phase x, f64, all n = nb + zs + zg columns (oracle/mp.py:rbf64)
+__device__ inline void rbf64(const DevCfg& c, double alpha_x, double bw, double x, double* phi) {
+  const int n = c.nb + c.zs + c.zg;
+  double cen[kMaxBasis + 4], e[kMaxBasis + 4];
+  for (int j = 0; j < n; ++j) {
+    const double u = (n > 1) ? (double)j / (double)(n - 1) : 0.0;
+    cen[j] = (c.phase == 0) ? u : exp((-alpha_x) * u);
+  }
+  for (int j = 0; j < n; ++j) {
+    double d = (n > 1) ? ((j < n - 1) ? cen[j + 1] - cen[j] : cen[n - 1] - cen[n - 2]) : 1.0;
+    const double h = bw / (d * d);
+    const double dd = x - cen[j];
+    e[j] = exp((-h) * (dd * dd) / 2);
+  }
+  double s;
+  if (n < 8) {
+    s = e[0] + 0.0;
+    for (int j = 1; j < n; ++j) s = s + e[j];
+  } else {   // numpy pairwise (8 accumulators, n <= 128)
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = e[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + e[i + j];
+    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) s = s + e[i];
+  }
+  for (int j = 0; j < n; ++j) phi[j] = e[j] / s;
+}
+
+// ProMP / DMP tables: one thread per row.
+__global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x, double bw, float* tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.rows) return;
+  double phi[kMaxBasis + 4];
+  const double t = (double)i * c.dt;
+  const double x = phase64(c, t, tau, delay, alpha_x);
+  rbf64(c, alpha_x, bw, x, phi);
+  float* row = tab + (size_t)i * c.stride;
+  if (c.mp == MP_PROMP) {
+    for (int j = 0; j < c.nb; ++j) row[j] = (float)(c.weights_scale * phi[c.zs + j]);
+    const float t0 = (float)t, t1 = (float)((double)(i + 1) * c.dt);
+    const float dt32 = t1 - t0;
+    row[c.nb] = dt32;
+    row[c.nb + 1] = 1.0f / dt32;     // RN(1/dt32) for div_rcp
+  } else {   // DMP: psi = x * phi ; sdt = f32(s_{i+1}) - f32(s_i)
+    for (int j = 0; j < c.nb; ++j) row[j] = (float)(x * phi[c.zs + j]);
+    double s0 = (t - delay) / tau, s1 = ((double)(i + 1) * c.dt - delay) / tau;
+    s0 = s0 > 0.0 ? s0 : 0.0;
+    s1 = s1 > 0.0 ? s1 : 0.0;
+    row[c.nb] = (float)s1 - (float)s0;
+  }
+}
+
+// ProDMP precompute (oracle/mp.py:prodmp_fine64).  Single block; scratch: [rows][2*nb] f64.
+__global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw, double* dp, float* tab) {
+  const int nb = c.nb, R = c.rows, W = 2 * nb;
+  const double h = c.dt / tau, a = c.alpha;
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    const double s = (double)i * h;
+    const double x = exp((-alpha_x) * s);
+    double phi[kMaxBasis + 4];
+    rbf64(c, alpha_x, bw, x, phi);
+    const double e = exp(a * s / 2);
+    const double k1 = s * e * x, k2 = e * x;
+    for (int j = 0; j < nb; ++j) {
+      dp[(size_t)i * W + j] = k1 * phi[c.zs + j];
+      dp[(size_t)i * W + nb + j] = k2 * phi[c.zs + j];
+    }
+  }
+  __syncthreads();
+  // cumulative trapezoid, one thread per column, sequential (same order as the oracle)
+  if ((int)threadIdx.x < W) {
+    const int j = threadIdx.x;
+    double p = 0.0, prev = dp[j];
+    dp[j] = 0.0;
+    for (int i = 1; i < R; ++i) {
+      const double cur = dp[(size_t)i * W + j];
+      p = p + h * (prev + cur) / 2;
+      dp[(size_t)i * W + j] = p;
+      prev = cur;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    const double s = (double)i * h;
+    const double e = exp(a * s / 2);
+    const double y1 = exp((-a) * s / 2);
+    const double y2 = s * y1;
+    const double dy1 = -a / 2 * y1;
+    const double dy2 = -a / 2 * y2 + y1;
+    const double q1 = (a * s / 2 - 1) * e + 1;
+    const double q2 = a / 2 * (e - 1);
+    float* row = tab + (size_t)i * c.stride;
+    for (int j = 0; j < nb; ++j) {
+      const double p1 = dp[(size_t)i * W + j], p2 = dp[(size_t)i * W + nb + j];
+      row[j] = (float)(p2 * y2 - p1 * y1);
+      row[nb + 1 + j] = (float)(p2 * dy2 - p1 * dy1);
+    }
+    row[nb] = (float)(q2 * y2 - q1 * y1);
+    row[2 * nb + 1] = (float)(q2 * dy2 - q1 * dy1);
+    row[2 * nb + 2] = (float)y1;
+    row[2 * nb + 3] = (float)y2;
+    row[2 * nb + 4] = (float)dy1;
+    row[2 * nb + 5] = (float)dy2;
+  }
+}
+
+}  // namespace fgx

@@ -239,12 +239,18 @@ class BlackBoxVectorEnv:
         return pos, vel
 
     # ------------------------------------------------------------------ fast path (bench)
-    def step_into(self, actions, obs, ret, te, tr, tl, fobs=None):
-        """Allocation-free BB step into preallocated buffers (no checks; for benchmarks)."""
+    def step_into(self, actions, obs, ret, te, tr, tl, fobs=None, inner_steps=None):
+        """Allocation-free BB step into preallocated buffers (no checks; for benchmarks).
+        inner_steps: optional int64 [1] device counter += sum of trajectory lengths."""
+        info = None
+        if inner_steps is not None:
+            info = _lib.FgxInfo()
+            info.inner_steps = inner_steps.data_ptr()
+            info = ctypes.byref(info)
         self._eng.lib.fgx_step(self._eng.h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
                                ctypes.c_void_p(ret.data_ptr()), ctypes.c_void_p(te.data_ptr()),
                                ctypes.c_void_p(tr.data_ptr()), ctypes.c_void_p(tl.data_ptr()),
-                               ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, None,
+                               ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, info,
                                int(self.autoreset), self._eng.stream())
 
     # ------------------------------------------------------------------ state / tables

@@ -125,6 +125,7 @@ typedef struct fgx_info {
   double* end_effector;  /* [N, T, 2] HoleReacher info                                     */
   double* reward_dist;   /* [N, T]  SimpleReacher info                                     */
   double* reward_ctrl;   /* [N, T]  SimpleReacher info                                     */
+  int64_t* inner_steps;  /* [1] += sum of trajectory_length over all envs (device counter)   */
 } fgx_info;
 
 const char* fgx_last_error(void);

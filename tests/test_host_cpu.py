@@ -33,6 +33,11 @@ def test_library_exports_every_declared_symbol():
     missing = declared - exported
     assert not missing, f"declared in include/fgx.h but not exported: {missing}"
     assert declared == set(_lib.EXPORTS), "ctypes binding out of sync with include/fgx.h"
+    # arity of every declaration == arity of the ctypes binding
+    for name in declared:
+        m = re.search(r"^\s*(?:int|const char\*)\s+" + name + r"\s*\(([^)]*)\)", header, re.S | re.M)
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(_lib.EXPORTS[name][1]), name
 
 
 def test_library_loads_and_reports_abi():
@@ -50,7 +55,7 @@ def test_library_loads_and_reports_abi():
 def test_config_struct_layout_matches_header():
     # 20 int32 then 18 doubles (see include/fgx.h)
     assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8
-    assert ctypes.sizeof(_lib.FgxInfo) == 10 * 8
+    assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
 
 
 def test_registry_ids():
