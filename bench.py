@@ -27,6 +27,33 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VEC_PEAK_TF = 78.6    # MI355X FP64 vector peak (spec; half the 157.3 TF FP32 vector peak)
 
 
+FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_k_episode.json")
+
+
+def episode_flops_per_step(env):
+    """Algorithmic flops of one inner env step of k_episode (PD controller, torque env).
+    f32: basis contraction (2 flop per fma) + velocity difference/division;
+    f64: PD (5 per dof), clip (0), Euler (4 per dof), control cost (2 per dof - 1), return (1)."""
+    n, nb = env.dof, 5
+    f32 = n * (2 * nb + 3)
+    f64 = n * 5 + n * 4 + (2 * n - 1) + 1
+    return f32, f64
+
+
+def pmc_traffic(env_id, n_envs):
+    """HBM bytes per k_episode launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 per the
+    gfx950 half-count correction + WRITE_SIZE, KiB -> B), if it was taken on this workload."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        if d.get("workload") == env_id and int(d.get("envs")) == n_envs:
+            return float(d["traffic_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def episode_bytes_per_env(env):
     """Algorithmic HBM bytes of one k_episode launch per env (info_level 0, autoreset on)."""
     n, P, out = env.dof, env.n_params, env.out_dim
@@ -150,6 +177,12 @@ def main():
 
     if rank == 0:
         value = inner / elapsed
+        f32f, f64f = episode_flops_per_step(env)
+        steps_per_s_kernel = (inner_local / K) / (kern_ms * 1e-3)
+        valu = {"f32_tflops": f32f * steps_per_s_kernel / 1e12, "f64_tflops": f64f * steps_per_s_kernel / 1e12,
+                "peak_f32_tflops": FP32_VEC_PEAK_TF, "peak_f64_tflops": FP64_VEC_PEAK_TF,
+                "frac": f32f * steps_per_s_kernel / 1e12 / FP32_VEC_PEAK_TF
+                + f64f * steps_per_s_kernel / 1e12 / FP64_VEC_PEAK_TF}
         bpe = episode_bytes_per_env(env)
         achieved = bpe * N / (kern_ms * 1e-3) / 1e9
         line = {
@@ -169,8 +202,12 @@ def main():
             "config": {"workload": args.env_id, "envs_per_gpu": N, "global_envs": N * world, "T": env.T,
                        "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_episode", "kernel_ms": kern_ms, "bytes_per_env": bpe},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.env_id, N),
+                         "kernel": "k_episode", "kernel_ms": kern_ms, "bytes_per_env": bpe,
+                         "bytes_per_inner_step": bpe * N / (inner_local / K),
+                         "note": "state lives in registers for all T substeps: the kernel is VALU-issue "
+                                 "bound (see valu); per-substep HBM design would need 242 B/step",
+                         "valu": valu},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

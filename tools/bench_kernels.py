@@ -1,0 +1,112 @@
+"""Per-kernel timing of every BASELINE config on one MI355X (diagnostics for DESIGN.md).
+
+Prints one JSON line per measurement: config, envs, kernel time (HIP events on the launch
+stream), inner env-steps/s, algorithmic bytes and GB/s where meaningful.
+"""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import fancy_gym_crowd_amd as fgx  # noqa: E402
+
+dev = torch.device("cuda", 0)
+
+
+def timed(fn, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3   # seconds per call
+
+
+def episode(env_id, N, over=None, label=None, reps=20):
+    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over)
+    env.reset(seed=0)
+    P = env.n_params
+    params = torch.from_numpy(np.random.default_rng(1234).standard_normal((N, P), dtype=np.float32)).to(dev)
+    obs = torch.empty((N, env.out_dim), device=dev)
+    fobs = torch.empty_like(obs)
+    ret = torch.empty(N, dtype=torch.float64, device=dev)
+    te = torch.empty(N, dtype=torch.uint8, device=dev)
+    tr = torch.empty(N, dtype=torch.uint8, device=dev)
+    tl = torch.empty(N, dtype=torch.int32, device=dev)
+    acc = torch.zeros(1, dtype=torch.int64, device=dev)
+    t = timed(lambda: env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc), reps=reps)
+    acc.zero_()
+    env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+    torch.cuda.synchronize()
+    inner = int(acc.item())
+    print(json.dumps(dict(kernel="k_episode", config=label or env_id, envs=N, kernel_us=t * 1e6,
+                          inner_steps_per_call=inner, inner_steps_per_s=inner / t,
+                          mean_traj_len=inner / N)), flush=True)
+
+
+def trajectory(env_id, N, force_valu=False):
+    over = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}} if force_valu else None
+    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over)
+    env.reset(seed=0)
+    params = torch.randn((N, env.n_params), device=dev)
+    T, n = env.T, env.dof
+    pos = torch.empty((N, T, n), device=dev)
+    vel = torch.empty_like(pos)
+    lib, h, s = env._eng.lib, env._eng.h, env._eng.stream()
+    import ctypes
+    args = [ctypes.c_void_p(x.data_ptr()) for x in (params, pos, vel)]
+    t = timed(lambda: lib.fgx_trajectory(h, *args, s))
+    bytes_ = N * (env.n_params * 4 + 2 * T * n * 4)
+    K = 8
+    flops = N * n * T * 2 * 2 * K          # two K=8 GEMMs (pos + next/vel) incl. zero padding
+    print(json.dumps(dict(kernel="k_traj_valu" if force_valu else "k_traj_mfma", config=env_id, envs=N,
+                          kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
+                          mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
+
+
+def step_raw(env_id, N):
+    env = fgx.make(env_id, num_envs=N, device=dev)
+    env.reset(seed=0)
+    n = env.dof
+    a = (torch.rand((N, n), device=dev) * 2 - 1) * 10
+    obs = torch.empty((N, env.obs_dim), device=dev)
+    rew = torch.empty(N, dtype=torch.float64, device=dev)
+    te = torch.empty(N, dtype=torch.uint8, device=dev)
+    tr = torch.empty(N, dtype=torch.uint8, device=dev)
+    import ctypes
+    lib, h, s = env._eng.lib, env._eng.h, env._eng.stream()
+    args = [ctypes.c_void_p(x.data_ptr()) for x in (a, obs, rew, te, tr)]
+    t = timed(lambda: lib.fgx_step_raw(h, *args, None, 1, s), reps=50)
+    # algorithmic bytes per env-step: action in, state r/w, obs out, reward, flags
+    state = 2 * n * 8 * 2 + 16 + 24 + 12 * 2
+    b = N * (n * 4 + state + env.obs_dim * 4 + 8 + 2)
+    print(json.dumps(dict(kernel="k_step_raw", config=env_id, envs=N, kernel_us=t * 1e6, steps_per_s=N / t,
+                          GBps=b / t / 1e9, hbm_frac=b / t / 8e12)), flush=True)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["episode", "traj", "raw"]
+    if "episode" in which:
+        episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
+        episode("fancy_ProMP/LongSimpleReacher-v0", 262144, label="ProMP LongSimpleReacher x4 envs")
+        episode("fancy_ProMP/SimpleReacher-v0", 4096, label="config2: ProMP SimpleReacher")
+        episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3: ProDMP HoleReacher", reps=5)
+        episode("fancy_DMP/LongSimpleReacher-v0", 32768, label="config4: DMP LongSimpleReacher (1/8 shard)")
+        episode("fancy_ProDMP/SimpleReacher-v0", 8192,
+                over={"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}},
+                label="config5: ProDMP SimpleReacher replan 25 (1/8 shard)")
+    if "traj" in which:
+        for force in (False, True):
+            trajectory("fancy_ProMP/LongSimpleReacher-v0", 65536, force)
+            trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
+    if "raw" in which:
+        step_raw("fancy/SimpleReacher-v0", 1 << 20)
+        step_raw("fancy/LongSimpleReacher-v0", 1 << 20)
+        step_raw("fancy/HoleReacher-v0", 1 << 20)
