@@ -147,7 +147,7 @@ struct PairwiseSum {
   }
   template <int J>
   __device__ __forceinline__ void add_ct(int k, double v, int split) {
-    if (split > 0 && k == split) first = comb(a);
+    if (J == 0 && split > 0 && k == split) first = comb(a);   // split % 8 == 0
     if (k < 128) push_ct<J>(a, t, k < 8, v);
     if (split > 0 && k >= split) push_ct<J>(b, u, k - split < 8, v);
   }

@@ -212,7 +212,7 @@ struct StepOut {
   bool coll, success;
 };
 
-template <int ENV, bool F32, int NL>
+template <int ENV, bool F32, int NL, bool MAYFK = true>
 __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const double* a, const float* a32,
                                            bool fk_always) {
   StepOut r;
@@ -238,8 +238,9 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
 #pragma unroll
       for (int d = 1; d < NL; ++d) ctrl = ctrl + a[d] * a[d];
     }
-    if (st >= 199 || fk_always) v.fk();
-    if (st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+    // MAYFK = false: the caller guarantees st < 199 (fast blocks), no FK code in the loop body
+    if (MAYFK && (st >= 199 || fk_always)) v.fk();
+    if (MAYFK && st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
     r.reward = r.rdist - ctrl;
     r.rctrl = ctrl;
   } else {
@@ -317,6 +318,10 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   if (MP != MP_GIVEN) tg.init(c, params + e * c.n_params, lds_tab, s0, ic_q, ic_qd);
 
   plans += 1;
+  // first sample index k with (k + 1 + s0) % replan == 0 (black_box_wrapper.py:233); the loop
+  // stops there unless max_planning_times is exhausted, in which case it never replans again
+  const int k_replan = (c.replan > 0 && (c.max_plans <= 0 || plans < c.max_plans))
+                           ? (c.replan - 1 - (s0 % c.replan)) : -1;
   PairwiseSum ps;
   ps.init();
   const int split = c.n_split;
@@ -341,11 +346,14 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // ---- tracking controller + clip (black_box_wrapper.py:201-205)
     double a[NL];
     float a32[NL];
+    bool nan_in = false;
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       if (CTRL == CTRL_PD) {
         const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
-        a[d] = np_clip(u, c.act_lo, c.act_hi);
+        a[d] = __builtin_fmin(__builtin_fmax(u, c.act_lo), c.act_hi);
+        nan_in |= (u != u);
+        if (LOG || J < 0) a[d] = (u != u) ? u : a[d];
         a32[d] = 0.0f;
       } else {
         const float u = (CTRL == CTRL_VEL) ? vel[d] : pos[d];
@@ -353,8 +361,16 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         a[d] = (double)a32[d];
       }
     }
+    // np.clip propagates NaN; max/min do not: fix up (rare, wave-uniform branch)
+    if (CTRL == CTRL_PD && !(LOG || J < 0) && __builtin_expect(__ballot(nan_in) != 0, 0)) {
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
+        if (u != u) a[d] = u;
+      }
+    }
     // ---- env.step
-    const StepOut r = substep<ENV, F32, NL>(c, v, a, a32, fk_always);
+    const StepOut r = substep<ENV, F32, NL, (J < 0)>(c, v, a, a32, fk_always);
     term = (ENV == ENV_HOLE) ? r.coll : false;
     trunc = v.steps >= c.max_steps;
     if constexpr (J >= 0) ps.template add_ct<J>(k, r.reward, split);
@@ -376,8 +392,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         o.reward_ctrl[ek] = r.rctrl;
       }
     }
-    const bool replan_now = c.replan > 0 && ((k + 1 + s0) % c.replan == 0) &&
-                            (c.max_plans <= 0 || plans < c.max_plans);
+    const bool replan_now = (k == k_replan);
     if (term || trunc || replan_now) {
       if (c.cond_desired) {
 #pragma unroll
@@ -389,16 +404,24 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     return false;
   };
 
-  int k = 0;
+  int k = 0;      // per-lane: index of the next sample
   if (!LOG) {
-    // fast path: blocks of 8 samples with compile-time return slots; SimpleReacher blocks
-    // never reach env step 199 (the only step whose reward needs FK)
-    while (!stop && k + 8 <= c.T && !(ENV == ENV_SIMPLE && v.steps + 8 > 199)) {
+    // fast path: blocks of 8 samples with compile-time return slots and a wave-uniform sample
+    // index.  SimpleReacher blocks must not reach env step 199 (the only step whose reward
+    // needs FK), so the wave runs the number of blocks every lane can take.
+    int nfast = c.T / 8;
+    if (ENV == ENV_SIMPLE) nfast = min(nfast, max(0, (199 - v.steps) / 8));
+    if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nfast = min(nfast, __shfl_xor(nfast, off, 64));
+    nfast = __builtin_amdgcn_readfirstlane(nfast);
+    for (int kb = 0; kb < 8 * nfast; kb += 8) {
 #define FGX_SAMPLE(J) \
-      if (!stop) { stop = sample(k, std::integral_constant<int, J>{}, false); ++k; }
+      if (!stop) { stop = sample(kb + J, std::integral_constant<int, J>{}, false); k = kb + J + 1; }
       FGX_SAMPLE(0) FGX_SAMPLE(1) FGX_SAMPLE(2) FGX_SAMPLE(3)
       FGX_SAMPLE(4) FGX_SAMPLE(5) FGX_SAMPLE(6) FGX_SAMPLE(7)
 #undef FGX_SAMPLE
+      if (__ballot(!stop) == 0) break;
     }
   }
   while (!stop && k < c.T) {

@@ -223,7 +223,10 @@ def test_bb_step_vs_oracle(ci):
         # other lengths (HoleReacher collisions in (128, 192)) agree to rounding only
         L_ = r_info["trajectory_length"]
         exact_ok = (L_ <= 128) | (L_ >= 192)
-        np.testing.assert_array_equal(np_(ret)[exact_ok], r_ret[exact_ok])
+        # (np.linalg.norm / np.dot go through the host BLAS: the kernel follows the OpenBLAS
+        # fma ordering pinned by the goldens; another host BLAS may round differently by an ulp)
+        g_, r_ = np_(ret)[exact_ok], r_ret[exact_ok]
+        assert np.all(np.abs(g_ - r_) <= 4 * np.spacing(np.abs(r_))), "returns beyond 4 ulp"
         n_exact += int((np_(ret) == r_ret).sum())
         close(np_(info["final_observation"]), r_info["final_obs"])
         close(np_(obs), r_obs)
