@@ -75,7 +75,8 @@ def cpu_baseline(seconds=12.0, cores=None):
         wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
     return dict(value=steps / wall, unit="inner env-steps/s", cores=cores, kind="port",
-                sample=f"oracle/port.py per-env loop (MP restatement + PD + 200 substeps + autoreset), "
+                sample=f"oracle/port.py per-env loop (f32 ProMP contraction + PD + 200 substeps with the "
+                       f"reference's per-step numpy ops incl. its 2 self-collision checks + autoreset), "
                        f"{WORKLOAD}, {cores} processes x ~{seconds:.0f}s, {steps} inner steps; "
                        f"os.cpu_count()={os.cpu_count()}, affinity={aff}")
 
@@ -87,9 +88,18 @@ def _cpu_worker(args):
     tables = mp.build_tables(spec, 202)
     rng = np.random.default_rng(1234 + wid)
 
+    phi = tables["phi"][1:201]                       # [T, nb] f32
+    dt32 = tables["dt32"][1:200, None]
+
     def traj(params, t0, q, qd):
-        p, v = mp.trajectory(spec, tables, params, int(round(t0 / 0.01)), q, qd)
-        return p[0], v[0]
+        # mp_pytorch-cost ProMP evaluation (one f32 contraction + forward difference per BB step);
+        # the bit-exact fma-chain emulation of oracle/mp.py is a checker, not a cost model
+        w = params.reshape(5, 5)
+        pos = (phi @ w.T).astype(np.float32)
+        vel = np.empty_like(pos)
+        vel[:-1] = (pos[1:] - pos[:-1]) / dt32
+        vel[-1] = vel[-2]
+        return pos, vel
     env = port.Reacher("LongSimpleReacher")
     bb = port.BlackBoxPort(env, traj, port.PD(0.6, 0.075), verbose=2)
     bb.reset(seed=wid)
@@ -117,20 +127,30 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal: more ranks than visible GPUs (the 1-GPU dev box) -> all ranks on cuda:0, gloo on
+    # host copies for the collectives; production: one rank per GPU, RCCL ("nccl") over xGMI
+    rehearsal = world > 1 and torch.cuda.device_count() < world
+    gpu = 0 if rehearsal else local
+    coll_dev = "cpu" if rehearsal else torch.device("cuda", gpu)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     import fancy_gym_crowd_amd as fgx
+    from fancy_gym_crowd_amd import shard
     N = args.envs
-    env = fgx.make(args.env_id, num_envs=N, device=dev, seed_offset=rank * N)
+    lo, _ = shard.shard_range(N, rank, world)
+    env = fgx.make(args.env_id, num_envs=N, device=dev, seed_offset=lo)
     P = env.n_params
     # MP parameters: default_rng(1234).standard_normal((N_global, P), f32), this rank's rows
     allp = np.random.default_rng(1234).standard_normal((N * world, P), dtype=np.float32)
-    params = torch.from_numpy(allp[rank * N:(rank + 1) * N]).to(dev)
+    params = torch.from_numpy(shard.shard_rows(allp, rank, world).copy()).to(dev)
     env.reset(seed=0)
     obs = torch.empty((N, env.out_dim), dtype=torch.float32, device=dev)
     fobs = torch.empty_like(obs)
@@ -157,8 +177,7 @@ def main():
         env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
         ev1[k].record()
     if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
-        gathered = [torch.empty_like(ret) for _ in range(world)]
-        dist.all_gather(gathered, ret)
+        all_ret = shard.gather_returns(ret.to(coll_dev))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -166,12 +185,9 @@ def main():
     inner_local = int(acc.item())
     kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([inner_local], dtype=torch.int64, device=dev)
-        dist.all_reduce(c)
-        inner = int(c.item())
+        elapsed = shard.max_over_ranks(elapsed, coll_dev)
+        inner = shard.sum_over_ranks(inner_local, coll_dev)
+        assert all_ret.numel() == N * world
     else:
         inner = inner_local
 
@@ -200,7 +216,8 @@ def main():
             "data": "synthetic: reset(seed=0) -> env i seeded with its global index; MP params "
                     "default_rng(1234).standard_normal((N_global, 25), f32)",
             "config": {"workload": args.env_id, "envs_per_gpu": N, "global_envs": N * world, "T": env.T,
-                       "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"},
+                       "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"
+                       + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.env_id, N),
                          "kernel": "k_episode", "kernel_ms": kern_ms, "bytes_per_env": bpe,
