@@ -278,12 +278,14 @@ class BatchedBB:
             acts_log = np.full((N, T, n), np.nan)
             obs_log = np.full((N, T, env.obs_dim + int(self.time_aware)), np.nan, f32)
             info_log = {}
-        a_is_f32 = self.ctrl[0] == "vel"
+        a_is_f32 = self.ctrl[0] in ("vel", "pos")
         for t in range(T):
             if self.ctrl[0] == "pd":
                 p, d = self.ctrl[1], self.ctrl[2]
                 a = p * (pos[:, t] - env.q) + d * (vel[:, t] - env.qd)
-            else:
+            elif self.ctrl[0] == "pos":          # pos_controller.py:8-9
+                a = pos[:, t]
+            else:                                 # vel_controller.py:8-9
                 a = vel[:, t]
             a = np.clip(a, env.act_low, env.act_high)
             o, r, te, tr, info = env.step(a if not a_is_f32 else a.astype(np.float64), act, a_is_f32)

@@ -83,3 +83,34 @@ def test_batched_vs_port_with_mp(ci):
             np.testing.assert_array_equal(inf["velocities"], info["velocities"][i])
             if t1 or t2:
                 np.testing.assert_array_equal(p.reset(), obs[i])
+
+
+def test_batched_vs_port_features():
+    """position controller, condition_on_desired and max_planning_times (replanning)."""
+    spec = mp.MPSpec("prodmp", 2, 5, "exp", 1.5, alpha=10.0)
+    cases = [("HoleReacher", ("pos",), mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1), 0, {}),
+             ("SimpleReacher", ("pd", 1.0, 0.1), spec, 25, dict(condition_on_desired=True)),
+             ("SimpleReacher", ("pd", 1.0, 0.1), spec, 25, dict(max_planning_times=3))]
+    for name, ctrl, sp, replan, kw in cases:
+        E = 5
+        bb = batched.BatchedBB(name, E, ctrl, mp_spec=sp, replan_period=replan, info_level=2, **kw)
+        tables = bb.tables
+        ports = []
+        for i in range(E):
+            env = port.Reacher(name)
+            fn = (lambda params, t0, cp, cv: tuple(
+                x[0] for x in mp.trajectory(sp, tables, params, int(round(t0 / 0.01)), cp, cv)))
+            c = {"pd": lambda: port.PD(ctrl[1], ctrl[2]), "vel": port.Vel, "pos": port.Pos}[ctrl[0]]()
+            ports.append(port.BlackBoxPort(env, fn, c, replan_period=replan, **kw))
+        np.testing.assert_array_equal(bb.reset(seed=3), np.array([p.reset(seed=3 + i) for i, p in enumerate(ports)]))
+        rng = np.random.default_rng(5)
+        for b in range(10 if replan else 3):
+            params = rng.standard_normal((E, sp.n_params), dtype=np.float32)
+            obs, ret, te, tr, info = bb.step(params)
+            for i, p in enumerate(ports):
+                o, r, t1, t2, inf = p.step(params[i])
+                assert r == ret[i] and t1 == te[i] and t2 == tr[i]
+                assert inf["trajectory_length"] == info["trajectory_length"][i]
+                np.testing.assert_array_equal(inf["positions"], info["positions"][i])
+                if t1 or t2:
+                    np.testing.assert_array_equal(p.reset(), obs[i])
