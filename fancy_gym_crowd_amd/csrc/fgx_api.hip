@@ -85,6 +85,8 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   if (c.ctrl_kind < FGX_CTRL_PD || c.ctrl_kind > FGX_CTRL_POS) return fail(FGX_E_INVALID, "bad ctrl_kind");
   if (c.mp_kind != FGX_MP_NONE) {
     if (c.T <= 0) return fail(FGX_E_INVALID, "T must be positive");
+    // the in-register return sum restates numpy's pairwise summation with one recursion level
+    if (c.T > 256) return fail(FGX_E_UNSUPPORTED, "plan length T > 256 not supported");
     if (c.n_basis != 5) return fail(FGX_E_UNSUPPORTED, "n_basis != 5 not instantiated");
     if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
@@ -139,6 +141,8 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     d.stride = (c.n_basis + 2 + 3) & ~3;   // [basis..., dt32 | sdt, rcp(dt32), pad] (16-B rows)
   }
   if (c.mp_kind == FGX_MP_NONE) { d.rows = 0; d.stride = 0; }
+  if ((int64_t)d.rows * d.stride * 4 > 64 * 1024)
+    return fail(FGX_E_UNSUPPORTED, "MP tables exceed 64 KiB of LDS (episode / replanning too long)");
   d.rand_width = std::isnan(c.hole_width);
   d.rand_x = std::isnan(c.hole_x);
   d.rand_depth = std::isnan(c.hole_depth);
@@ -152,6 +156,8 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.act_lo32 = (float)c.act_low;
   d.act_hi32 = (float)c.act_high;
   d.dt32 = (float)c.dt;
+  d.rcp_dt = 1.0 / c.dt;          // RN(1/dt): div_rcp64 (Markstein) is exact with it
+  d.rcp_dt32 = 1.0f / d.dt32;
   d.tau32 = (float)c.tau;
   d.rcp_tau32 = 1.0f / d.tau32;
   d.hole_w0 = c.hole_width;

@@ -39,8 +39,8 @@ struct DevCfg {
   int rand_width, rand_x, rand_depth;
   int n_split;      // numpy pairwise split point for a T-long return sum (0: none)
   int ctx_idx[kMaxObs + 1];
-  double dt, tau, p_gain, d_gain, act_lo, act_hi;
-  float act_lo32, act_hi32, dt32, tau32, rcp_tau32;
+  double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;
+  float act_lo32, act_hi32, dt32, rcp_dt32, tau32, rcp_tau32;
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
   float ws32, gs32, alpha32, beta32;
   double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
@@ -106,6 +106,12 @@ __device__ __forceinline__ float div_rcp(float x, float d, float r) {
   const float q = x * r;
   const float e = __builtin_fmaf(-q, d, x);
   return __builtin_fmaf(e, r, q);
+}
+
+__device__ __forceinline__ double div_rcp64(double x, double d, double r) {
+  const double q = x * r;
+  const double e = __builtin_fma(-q, d, x);
+  return __builtin_fma(e, r, q);
 }
 
 // np.linalg.norm of a 2-vector == sqrt(ddot) == sqrt(fma(y, y, x*x)) (OpenBLAS order)
@@ -303,6 +309,7 @@ struct Env {
       const double y0 = jy[k], y1 = jy[k + 1];
       if (y0 >= 0.0 && y1 >= 0.0 && nd <= 0.0) continue;
       const double bx = jx[k], by = jy[k], ck = c[k], sk = s[k];
+#pragma unroll 4
       for (int j = 0; j < 100; ++j) {
         const double px = ck * cf.lin[j] + bx;
         const double py = sk * cf.lin[j] + by;

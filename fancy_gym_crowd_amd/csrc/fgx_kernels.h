@@ -249,7 +249,7 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       float s32 = 0.0f;
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        const float ac = (a32[d] - (float)v.qd[d]) / c.dt32;
+        const float ac = div_rcp(a32[d] - (float)v.qd[d], c.dt32, c.rcp_dt32);
         s32 = (d == 0) ? ac * ac : s32 + ac * ac;
       }
       acc_cost = (double)s32;
@@ -257,7 +257,7 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       acc_cost = 0.0;
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        const double ac = (a[d] - v.qd[d]) / c.dt;
+        const double ac = div_rcp64(a[d] - v.qd[d], c.dt, c.rcp_dt);
         acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
       }
     }
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   };
 
   int k = 0;      // per-lane: index of the next sample
-  if (!LOG) {
+  if (!LOG && ENV == ENV_SIMPLE) {   // (HoleReacher's FK + collision body is too large to unroll)
     // fast path: blocks of 8 samples with compile-time return slots and a wave-uniform sample
     // index.  SimpleReacher blocks must not reach env step 199 (the only step whose reward
     // needs FK), so the wave runs the number of blocks every lane can take.

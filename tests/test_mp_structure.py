@@ -74,3 +74,19 @@ def test_division_by_reciprocal_is_exact():
     for d in divisors:
         d32 = np.float32(d)
         np.testing.assert_array_equal(_div_rcp(x, d32), (x / d32).astype(np.float32))
+
+
+def test_f64_division_by_reciprocal_is_exact():
+    """div_rcp64 (fgx_device.h) for the env dt: RN(x / 0.01) == fma(fma(-q, d, x), r, q)."""
+    from fractions import Fraction as F
+
+    def fma(a, b, c):
+        return float(F(a) * F(b) + F(c))
+    d = 0.01
+    r = 1.0 / d
+    rng = np.random.default_rng(7)
+    xs = list(rng.standard_normal(4000) * rng.choice([1e-6, 1e-3, 1.0, 1e3, 1e6], 4000))
+    xs += [i * 0.01 for i in range(1, 500)] + [float(i) for i in range(1, 500)]
+    for x in xs:
+        q = x * r
+        assert fma(fma(-q, d, x), r, q) == x / d, x
