@@ -144,18 +144,13 @@ struct PairwiseSum {
     if (j == 7) tail = comb(r);
     else tail = tail + v;
   }
-  // compile-time slot J == k & 7 (the caller unrolls its loop by 8)
-  template <int J>
-  __device__ __forceinline__ static void push_ct(double* r, double& tail, bool first_block, double v) {
-    r[J] = first_block ? v : r[J] + v;
-    if (J == 7) tail = comb(r);
-    else tail = tail + v;
-  }
-  template <int J>
-  __device__ __forceinline__ void add_ct(int k, double v, int split) {
-    if (J == 0 && split > 0 && k == split) first = comb(a);   // split % 8 == 0
-    if (k < 128) push_ct<J>(a, t, k < 8, v);
-    if (split > 0 && k >= split) push_ct<J>(b, u, k - split < 8, v);
+  // Unrolled fast loop: compile-time slot J == k & 7 and a block-uniform phase PH (bit 0: the
+  // sample is in [0, 128), bit 1: in [split, T)).  The accumulators start at 0, so 0 + v == v
+  // replaces numpy's first-block copy (only the sign of an all-zero partial sum can differ).
+  template <int J, int PH>
+  __device__ __forceinline__ void add_fast(double v) {
+    if (PH & 1) { a[J] = a[J] + v; t = (J == 7) ? comb(a) : t + v; }
+    if (PH & 2) { b[J] = b[J] + v; u = (J == 7) ? comb(b) : u + v; }
   }
   __device__ __forceinline__ void add(int k, double v, int split) {
     if (split > 0 && k == split) first = comb(a);   // blocks [0, split) only

@@ -332,8 +332,11 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   // One plan sample k: desired state -> controller -> clip -> env.step -> return / info.
   // J = k & 7 when known at compile time (unrolled fast loop), -1 otherwise.  Returns true
   // when the BB step ends after this sample (black_box_wrapper.py:233-239).
-  auto sample = [&](int k, auto Jtag, bool fk_always) -> bool {
+  // canonical clip bounds: v_max/v_min need no per-sample canonicalisation of kernel args
+  const double act_lo = __builtin_canonicalize(c.act_lo), act_hi = __builtin_canonicalize(c.act_hi);
+  auto sample = [&](int k, auto Jtag, auto PHtag, bool fk_always) -> bool {
     constexpr int J = decltype(Jtag)::value;
+    constexpr int PH = decltype(PHtag)::value;
     if (MP == MP_GIVEN) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     for (int d = 0; d < NL; ++d) {
       if (CTRL == CTRL_PD) {
         const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
-        a[d] = __builtin_fmin(__builtin_fmax(u, c.act_lo), c.act_hi);
+        a[d] = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
         nan_in |= (u != u);
         if (LOG || J < 0) a[d] = (u != u) ? u : a[d];
         a32[d] = 0.0f;
@@ -371,10 +374,14 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
     // ---- env.step
     const StepOut r = substep<ENV, F32, NL, (J < 0)>(c, v, a, a32, fk_always);
-    term = (ENV == ENV_HOLE) ? r.coll : false;
-    trunc = v.steps >= c.max_steps;
-    if constexpr (J >= 0) ps.template add_ct<J>(k, r.reward, split);
-    else ps.add(k, r.reward, split);
+    if constexpr (J >= 0) {   // fast blocks: no termination, truncation or replanning inside
+      ps.template add_fast<J, PH>(r.reward);
+      return false;
+    } else {
+      term = (ENV == ENV_HOLE) ? r.coll : false;
+      trunc = v.steps >= c.max_steps;
+      ps.add(k, r.reward, split);
+    }
     // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
     if (LOG) {
       const int64_t ek = e * c.T + k;
@@ -407,25 +414,32 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   int k = 0;      // per-lane: index of the next sample
   if (!LOG && ENV == ENV_SIMPLE) {   // (HoleReacher's FK + collision body is too large to unroll)
     // fast path: blocks of 8 samples with compile-time return slots and a wave-uniform sample
-    // index.  SimpleReacher blocks must not reach env step 199 (the only step whose reward
-    // needs FK), so the wave runs the number of blocks every lane can take.
-    int nfast = c.T / 8;
-    if (ENV == ENV_SIMPLE) nfast = min(nfast, max(0, (199 - v.steps) / 8));
+    // index.  Fast samples must not reach env step 199 (the only SimpleReacher step whose reward
+    // needs FK), the TimeLimit or the replanning sample, so no lane leaves the loop early and
+    // the blocks carry no per-lane control flow; the wave runs the blocks every lane can take.
+    int lim = min(199, c.max_steps - 1) - v.steps;
+    if (k_replan >= 0) lim = min(lim, k_replan);
+    int nfast = min(c.T, max(0, lim)) / 8;
     if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nfast = min(nfast, __shfl_xor(nfast, off, 64));
     nfast = __builtin_amdgcn_readfirstlane(nfast);
     for (int kb = 0; kb < 8 * nfast; kb += 8) {
-#define FGX_SAMPLE(J) \
-      if (!stop) { stop = sample(kb + J, std::integral_constant<int, J>{}, false); k = kb + J + 1; }
-      FGX_SAMPLE(0) FGX_SAMPLE(1) FGX_SAMPLE(2) FGX_SAMPLE(3)
-      FGX_SAMPLE(4) FGX_SAMPLE(5) FGX_SAMPLE(6) FGX_SAMPLE(7)
+      if (split > 0 && kb == split) ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
+      // phase of this block (uniform): pushes into the level-1 and/or second-half sums
+      const int ph = (kb < 128 ? 1 : 0) | ((split > 0 && kb >= split) ? 2 : 0);
+#define FGX_SAMPLE(J, PH) sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}, false);
+#define FGX_BLOCK(PH) \
+      FGX_SAMPLE(0, PH) FGX_SAMPLE(1, PH) FGX_SAMPLE(2, PH) FGX_SAMPLE(3, PH) \
+      FGX_SAMPLE(4, PH) FGX_SAMPLE(5, PH) FGX_SAMPLE(6, PH) FGX_SAMPLE(7, PH)
+      if (ph == 1) { FGX_BLOCK(1) } else if (ph == 3) { FGX_BLOCK(3) } else { FGX_BLOCK(2) }
+#undef FGX_BLOCK
 #undef FGX_SAMPLE
-      if (__ballot(!stop) == 0) break;
     }
+    k = 8 * nfast;
   }
   while (!stop && k < c.T) {
-    stop = sample(k, std::integral_constant<int, -1>{}, LOG);
+    stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG);
     ++k;
   }
   k -= 1;   // index of the last executed sample

@@ -266,6 +266,51 @@ def test_bb_step_vs_oracle(ci):
     assert n_exact >= 0.8 * N * n_bb, f"only {n_exact} returns bit-exact"
 
 
+FAST = FULL + [
+    ("fancy_DMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}}, 256, 8),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(64)}}, 192, 6),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(FAST)))
+def test_bb_fast_path_vs_oracle(ci):
+    """info_level 0 runs the unrolled fast loop (fgx_kernels.h k_episode): returns, flags, lengths,
+    observations and the full f64 env state after every BB step.  After the first step every
+    third env is reset (unseeded, reset_mask) so that lanes of one wave sit at different env
+    steps and replanning phases, which the wave-uniform fast-block count must respect."""
+    env_id, over, N, n_bb = FAST[ci]
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    spec = spec_of(env)
+    name = NAME[env_id.split("/")[1]]
+    ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec, info_level=0,
+                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+    close(np_(env.reset(seed=2000)[0]), ob.reset(seed=2000))
+    rng = np.random.default_rng(91)
+    n_exact = 0
+    for b in range(n_bb):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        np.testing.assert_array_equal(np_(te), r_te)
+        np.testing.assert_array_equal(np_(tr), r_tr)
+        close(np_(ret), r_ret)
+        n_exact += int((np_(ret) == r_ret).sum())
+        close(np_(info["final_observation"]), r_info["final_obs"])
+        close(np_(obs), r_obs)
+        st = env.get_state()
+        np.testing.assert_array_equal(np_(st["q"]), ob.env.q)
+        np.testing.assert_array_equal(np_(st["qd"]), np.asarray(ob.env.qd, np.float64))
+        np.testing.assert_array_equal(np_(st["steps"]), ob.env.steps)
+        if b == 0:
+            mask = np.zeros(N, np.uint8)
+            mask[::3] = 1
+            o_g, _ = env.reset(options={"reset_mask": torch.from_numpy(mask)})
+            o_r = ob._reset_idx([i for i in range(N) if mask[i]])
+            close(np_(o_g)[mask == 1], o_r)
+    assert n_exact >= 0.8 * N * n_bb, f"only {n_exact} returns bit-exact"
+
+
 def test_step_based_golden():
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "step_based.npz"))
     for kind, name in (("simple", "fancy/SimpleReacher-v0"), ("long", "fancy/LongSimpleReacher-v0"),
