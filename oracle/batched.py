@@ -16,15 +16,28 @@ f32 = np.float32
 DT32 = f32(0.01)
 
 
+def _seqsum(sq, as32):
+    """np.sum over the last axis of a [N, n<8] array: left-to-right (f32 when as32)."""
+    if as32:
+        c = sq[:, 0].astype(f32)
+        for j in range(1, sq.shape[1]):
+            c = (c + sq[:, j]).astype(f32)
+        return c
+    c = sq[:, 0] + 0.0
+    for j in range(1, sq.shape[1]):
+        c = c + sq[:, j]
+    return c
+
+
 def _norm2(v):
     """np.linalg.norm of each row of a [M, 2] array (per-row call: BLAS ordering kept)."""
     return np.array([np.linalg.norm(r) for r in v], dtype=np.float64)
 
 
 class BatchedReacher:
-    def __init__(self, name, N, random_start=True):
+    def __init__(self, name, N, random_start=None, **overrides):
         self.N = N
-        self.envs = [Reacher(name, random_start) for _ in range(N)]   # RNG + reset sampling
+        self.envs = [Reacher(name, random_start, **overrides) for _ in range(N)]   # RNG + reset sampling
         e0 = self.envs[0]
         self.kind, self.n, self.dt = e0.kind, e0.n, e0.dt
         self.obs_dim = e0.obs_dim
@@ -41,6 +54,14 @@ class BatchedReacher:
             self.hole_w = np.zeros(N)
             self.hole_d = float(e0.init_depth)
             self.rew_factors = e0.rew_factors
+            self.rew_fct = e0.rew_fct
+            self.allow_self, self.allow_wall = e0.allow_self, e0.allow_wall
+            self.rf_collided = np.zeros(N, bool)      # vel_acc reward function state
+            self.rf_coll_dist = np.zeros(N)
+            self.ee_save = np.zeros((N, 2))           # unbounded reward function state
+        if self.kind == "via":
+            self.via = np.zeros((N, 2))
+            self.allow_self, self.penalty = e0.allow_self, e0.penalty
 
     def reset(self, idx, seeds=None):
         """Reset envs idx (list); returns obs [len(idx), obs_dim] f32."""
@@ -55,6 +76,10 @@ class BatchedReacher:
             self.steps[i] = 0
             if self.kind == "hole":
                 self.hole_x[i], self.hole_w[i] = e.hole_x, e.hole_w
+                self.rf_collided[i] = False
+                self.rf_coll_dist[i] = 0.0
+            if self.kind == "via":
+                self.via[i] = e.via
             out.append(o)
         self._fk()
         return np.array(out, dtype=f32).reshape(len(idx), self.obs_dim)
@@ -72,6 +97,8 @@ class BatchedReacher:
         cols = [np.cos(self.q), np.sin(self.q), self.qd]
         if self.kind == "hole":
             cols.append(self.hole_w[:, None])
+        if self.kind == "via":
+            cols.append(self.ee - self.via)
         cols += [self.ee - self.goal, self.steps[:, None].astype(np.float64)]
         return np.concatenate(cols, axis=1).astype(f32)
 
@@ -166,34 +193,85 @@ class BatchedReacher:
             info["reward_dist"] = dist
             info["reward_ctrl"] = ctrl
             term = np.zeros(N, bool)
+        elif self.kind == "via":
+            coll = np.zeros(N, bool) if self.allow_self else self._self_collision()
+            if a_is_f32:   # 5e-8 * float32 scalar stays float32 (NEP 50)
+                pen_ctrl = (f32(5e-8) * _seqsum(a.astype(f32) ** 2, True)).astype(f32).astype(np.float64)
+            else:
+                pen_ctrl = 5e-8 * _seqsum(a ** 2, False)
+            reward = np.full(N, -np.inf)
+            success = np.zeros(N, bool)
+            for i in np.nonzero(act)[0]:
+                if coll[i]:
+                    d = np.linalg.norm(self.ee[i] - self.goal[i])
+                    reward[i] = (-self.penalty - d ** 2) - pen_ctrl[i]
+                elif steps[i] == 100:
+                    success[i] = np.linalg.norm(self.ee[i] - self.via[i]) < 0.005
+                elif steps[i] == 199:
+                    success[i] = np.linalg.norm(self.ee[i] - self.goal[i]) < 0.005
+            info["is_success"] = success
+            info["is_collided"] = coll
+            info["end_effector"] = self.ee.copy()
+            term = coll
         else:
-            coll = self._self_collision() | self._wall_collision()
             if a_is_f32:
-                sq32 = (acc32 * acc32).astype(f32)
-                c32 = sq32[:, 0].astype(f32)
-                for j in range(1, n):
-                    c32 = (c32 + sq32[:, j]).astype(f32)
                 sq64 = acc64 * acc64
-                c64 = sq64[:, 0] + 0.0
-                for j in range(1, n):
-                    c64 = c64 + sq64[:, j]
-                acc_cost = np.where(use32, c32.astype(np.float64), c64)
+                acc_cost = np.where(use32, _seqsum((acc32 * acc32).astype(f32), True).astype(np.float64),
+                                    _seqsum(sq64, False))
                 self.qd_f32 = np.where(act, True, self.qd_f32)
             else:
-                sq64 = acc64 * acc64
-                acc_cost = sq64[:, 0] + 0.0
-                for j in range(1, n):
-                    acc_cost = acc_cost + sq64[:, j]
-            special = act & ((steps == 199) | coll)
-            reward = acc_cost * self.rew_factors[1]      # fma(0,-100,fma(acc,-5e-8,-0.0))
+                acc_cost = _seqsum(acc64 * acc64, False)
             success = np.zeros(N, bool)
-            if np.any(special):
-                idx = np.nonzero(special)[0]
-                dist = _norm2(self.ee[idx] - self.goal[idx])
-                for j, i in enumerate(idx):
-                    feats = np.array((dist[j] ** 2, acc_cost[i], int(coll[i])))
-                    reward[i] = np.dot(feats, self.rew_factors)
-                    success[i] = dist[j] < 0.005 and not coll[i]
+            if self.rew_fct == "simple":
+                coll = ((np.zeros(N, bool) if self.allow_self else self._self_collision())
+                        | (np.zeros(N, bool) if self.allow_wall else self._wall_collision()))
+                special = act & ((steps == 199) | coll)
+                reward = acc_cost * self.rew_factors[1]      # fma(0,-100,fma(acc,-5e-8,-0.0))
+                if np.any(special):
+                    idx = np.nonzero(special)[0]
+                    dist = _norm2(self.ee[idx] - self.goal[idx])
+                    for j, i in enumerate(idx):
+                        feats = np.array((dist[j] ** 2, acc_cost[i], int(coll[i])))
+                        reward[i] = np.dot(feats, self.rew_factors)
+                        success[i] = dist[j] < 0.005 and not coll[i]
+            elif self.rew_fct == "vel_acc":
+                # qd after the step is the action (float32 values when a_is_f32)
+                vel_cost = (_seqsum(a.astype(f32) ** 2, True).astype(np.float64) if a_is_f32
+                            else _seqsum(a ** 2, False))
+                fresh = act & ~self.rf_collided
+                now = ((np.zeros(N, bool) if self.allow_self else self._self_collision())
+                       | (np.zeros(N, bool) if self.allow_wall else self._wall_collision()))
+                self.rf_collided = np.where(fresh, now, self.rf_collided)
+                for i in np.nonzero(fresh)[0]:
+                    self.rf_coll_dist[i] = np.linalg.norm(self.ee[i] - self.goal[i])
+                coll = self.rf_collided.copy()
+                reward = np.zeros(N)
+                for i in np.nonzero(act)[0]:
+                    dist_cost, collision_cost, time_cost = 0, 0, 0
+                    if steps[i] == 199:
+                        dist = np.linalg.norm(self.ee[i] - self.goal[i])
+                        success[i] = dist < 0.005 and not coll[i]
+                        dist_cost = dist ** 2
+                        collision_cost = coll[i] * self.rf_coll_dist[i] ** 2
+                        time_cost = 199 - int(steps[i])
+                    reward[i] = np.dot(np.array((dist_cost, vel_cost[i], acc_cost[i], collision_cost, time_cost)),
+                                       self.rew_factors)
+            else:   # unbounded
+                coll = ((np.zeros(N, bool) if self.allow_self else self._self_collision())
+                        | (np.zeros(N, bool) if self.allow_wall else self._wall_collision()))
+                save = act & ((steps == 180) | coll)
+                self.ee_save = np.where(save[:, None], self.ee, self.ee_save)
+                reward = acc_cost * self.rew_factors[1]      # fma(acc, -5e-6, 0 * 1)
+                for i in np.nonzero(act & ((steps == 199) | coll))[0]:
+                    dist = np.linalg.norm(self.ee_save[i] - self.goal[i])
+                    if coll[i]:
+                        dr = 0.25 * np.exp(-dist)
+                    elif self.ee[i, 1] > 0:
+                        dr = np.exp(-dist)
+                    else:
+                        dr = 1 - self.ee_save[i, 1]
+                    success[i] = not coll[i]
+                    reward[i] = np.dot(np.array((dr, acc_cost[i])), self.rew_factors)
             info["is_success"] = success
             info["is_collided"] = coll
             info["end_effector"] = self.ee.copy()
@@ -212,8 +290,8 @@ class BatchedBB:
 
     def __init__(self, name, N, ctrl, mp_spec=None, traj_fn=None, replan_period=0,
                  max_planning_times=np.inf, condition_on_desired=False, info_level=0,
-                 time_aware=None, tables=None):
-        self.env = BatchedReacher(name, N)
+                 time_aware=None, tables=None, env_kwargs=None):
+        self.env = BatchedReacher(name, N, **(env_kwargs or {}))
         self.N = N
         self.ctrl = ctrl
         self.spec = mp_spec

@@ -22,11 +22,12 @@ What this does
   desired trajectory* (env, controller, clip, BB loop, replanning bookkeeping,
   TimeAwareObservation, reset RNG streams).
 
-Outputs (small .npz files, all < 1 MB together):
+Outputs (small .npz files):
     resets.npz, step_based.npz, bb_simple.npz, bb_long.npz, bb_hole_vel.npz,
-    bb_hole_pd.npz, bb_replan.npz
+    bb_hole_pd.npz, bb_replan.npz                     ("base")
+    variants.npz  ViaPointReacher + HoleReacher rew_fct vel_acc / unbounded ("variants")
 
-Run:  python tests/golden/make_golden.py   (needs /root/reference; not on the GPU box)
+Run:  python tests/golden/make_golden.py [base] [variants]   (needs /root/reference; not on the GPU box)
 """
 import os
 import sys
@@ -190,6 +191,8 @@ from fancy_gym.envs.classic_control.simple_reacher.simple_reacher import SimpleR
 from fancy_gym.envs.classic_control.simple_reacher.mp_wrapper import MPWrapper as SRMPWrapper  # noqa: E402
 from fancy_gym.envs.classic_control.hole_reacher.hole_reacher import HoleReacherEnv  # noqa: E402
 from fancy_gym.envs.classic_control.hole_reacher.mp_wrapper import MPWrapper as HRMPWrapper  # noqa: E402
+from fancy_gym.envs.classic_control.viapoint_reacher.viapoint_reacher import ViaPointReacherEnv  # noqa: E402
+from fancy_gym.envs.classic_control.viapoint_reacher.mp_wrapper import MPWrapper as VPMPWrapper  # noqa: E402
 from fancy_gym.black_box.black_box_wrapper import BlackBoxWrapper  # noqa: E402
 from fancy_gym.black_box.controller.pd_controller import PDController  # noqa: E402
 from fancy_gym.black_box.controller.vel_controller import VelController  # noqa: E402
@@ -206,10 +209,13 @@ def make_raw(kind):
         env = SimpleReacherEnv(n_links=2)
     elif kind == "long":
         env = SimpleReacherEnv(n_links=5)
-    elif kind == "hole":
+    elif kind.startswith("hole"):
+        rew = {"hole": "simple", "hole_velacc": "vel_acc", "hole_unbounded": "unbounded"}[kind]
         env = HoleReacherEnv(n_links=5, random_start=True, allow_self_collision=False,
                              allow_wall_collision=False, hole_width=None, hole_depth=1,
-                             hole_x=None, collision_penalty=100)
+                             hole_x=None, collision_penalty=100, rew_fct=rew)
+    elif kind == "via":   # envs/__init__.py:669-679
+        env = ViaPointReacherEnv(n_links=5, allow_self_collision=False, collision_penalty=1000)
     else:
         raise ValueError(kind)
     env.spec = _Spec()
@@ -340,16 +346,17 @@ def gen_step_based():
 
 
 # ----------------------------------------------------------------------------- (iii)/(iv) BB
-def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True):
+def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True, out_dict=None):
     """E envs, reset(seed=100+i), n_bb BB steps each with autoreset; stub MP tables per (env, bb)."""
     rng = np.random.default_rng(4321)
+    wrap = {"via": VPMPWrapper}.get(kind, HRMPWrapper if kind.startswith("hole") else SRMPWrapper)
     dof = 2 if kind == "simple" else 5
     recs = {k: [] for k in ("pos", "vel", "obs", "ret", "term", "trunc", "tlen", "actions",
                             "step_obs", "step_rew", "reset_obs", "obs0", "init_time", "init_pos",
                             "init_vel", "info_a", "info_b", "info_ee")}
     for i in range(E):
         raw = make_raw(kind)
-        env = SRMPWrapper(raw) if kind != "hole" else HRMPWrapper(raw)
+        env = wrap(raw)
         if replan is not None:
             env = TimeAwareObservation(env)
         n_rows = 400 if replan is not None else 200
@@ -374,7 +381,7 @@ def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True):
             per["actions"].append(pad(info["step_actions"], dof))
             per["step_obs"].append(pad(info["step_observations"], info["step_observations"].shape[-1], np.float32))
             per["step_rew"].append(pad(info["step_rewards"], 1)[:, 0])
-            if kind == "hole":
+            if kind != "simple" and kind != "long":
                 per["info_a"].append(pad(np.array(info["is_collided"], dtype=float), 1)[:, 0])
                 per["info_b"].append(pad(np.array(info["is_success"], dtype=float), 1)[:, 0])
                 per["info_ee"].append(pad(np.array(info["end_effector"]), 2))
@@ -392,6 +399,9 @@ def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True):
         for k, v in per.items():
             recs[k].append(v)
     out = {k: np.array(v) for k, v in recs.items()}
+    if out_dict is not None:
+        out_dict.update({f"{name}_{k}": v for k, v in out.items()})
+        return
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
 
 
@@ -420,10 +430,70 @@ def gen_bb():
            replan=lambda pos, vel, obs, action, t: t % 25 == 0)
 
 
+# ----------------------------------------------------------------------------- (vi) widening
+def gen_variants():
+    """ViaPointReacher (envs/__init__.py:669-679) and the HoleReacher reward variants
+    (hole_reacher.py:48-58: rew_fct "vel_acc" / "unbounded"): resets, step-based rollouts and
+    BB steps given a desired trajectory, in one file."""
+    out = {}
+    env = make_raw("via")
+    u = env.unwrapped
+    rec = {k: [] for k in ("q0", "via", "goal", "obs", "cont_via", "cont_goal", "cont_obs")}
+    for s in range(64):
+        o, _ = env.reset(seed=s)
+        rec["q0"].append(u._joint_angles.copy()); rec["via"].append(np.array(u._via_point, np.float64))
+        rec["goal"].append(np.array(u._goal, np.float64)); rec["obs"].append(o)
+        cv, cg, co = [], [], []
+        for _ in range(3):
+            o2, _ = env.reset()
+            cv.append(np.array(u._via_point, np.float64)); cg.append(np.array(u._goal, np.float64)); co.append(o2)
+        rec["cont_via"].append(cv); rec["cont_goal"].append(cg); rec["cont_obs"].append(co)
+    out.update({f"viareset_{k}": np.array(v) for k, v in rec.items()})
+    for kind, E in (("via", 4), ("hole_velacc", 4), ("hole_unbounded", 4)):
+        rng = np.random.default_rng(99)
+        acts = rng.uniform(-0.35 * 2 * np.pi, 0.35 * 2 * np.pi, (200, E, 5)) + rng.uniform(-2.0, 2.0, (1, E, 5))
+        acts = acts.astype(np.float32)
+        envs = [make_raw(kind) for _ in range(E)]
+        obs0 = np.array([e.reset(seed=i)[0] for i, e in enumerate(envs)])
+        O, R, TE, TR, RESET = [], [], [], [], []
+        for t in range(200):
+            o_t, r_t, te_t, tr_t, rs_t = [], [], [], [], []
+            for i, e in enumerate(envs):
+                o, r, te, tr, _ = e.step(acts[t, i])
+                o_t.append(o); r_t.append(float(r)); te_t.append(bool(te)); tr_t.append(bool(tr))
+                rs_t.append(e.reset()[0] if (te or tr) else np.full_like(o, np.nan))
+            O.append(o_t); R.append(r_t); TE.append(te_t); TR.append(tr_t); RESET.append(rs_t)
+        out[f"{kind}_actions"] = acts
+        out[f"{kind}_obs0"] = obs0
+        out[f"{kind}_obs"] = np.array(O, dtype=np.float32)
+        out[f"{kind}_rew"] = np.array(R)
+        out[f"{kind}_term"] = np.array(TE)
+        out[f"{kind}_trunc"] = np.array(TR)
+        out[f"{kind}_reset_obs"] = np.array(RESET, dtype=np.float32)
+
+    def vel_tab(rng, n, dof):
+        return smooth_tables(rng, n, dof, 0.5, 1.2)
+
+    def fold_tab(rng, n, dof):
+        off = rng.uniform(-3.5, 3.5, dof)
+        off[0] = rng.uniform(0.0, np.pi)
+        return smooth_tables(rng, n, dof, 0.6, 1.0, offset=off)
+
+    # ViaPointReacher ProMP/DMP: velocity controller (viapoint_reacher/mp_wrapper.py:11-23)
+    run_bb("bbvia", "via", VelController(), 4, 2, vel_tab, out_dict=out)
+    run_bb("bbvelacc", "hole_velacc", PDController(1.0, 0.1), 4, 2, fold_tab, out_dict=out)
+    run_bb("bbunb", "hole_unbounded", VelController(), 4, 2, vel_tab, out_dict=out)
+    np.savez_compressed(os.path.join(OUT, "variants.npz"), **out)
+
+
 if __name__ == "__main__":
-    gen_resets()
-    gen_step_based()
-    gen_bb()
+    which = sys.argv[1:] or ["base", "variants"]
+    if "base" in which:
+        gen_resets()
+        gen_step_based()
+        gen_bb()
+    if "variants" in which:
+        gen_variants()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
