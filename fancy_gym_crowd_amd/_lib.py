@@ -11,8 +11,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 1
-ENV_SIMPLE, ENV_HOLE = 0, 1
+FGX_ABI_VERSION = 2
+ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
+REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
 MP_NONE, MP_PROMP, MP_DMP, MP_PRODMP = 0, 1, 2, 3
 PHASE_LINEAR, PHASE_EXP = 0, 1
 CTRL_PD, CTRL_VEL, CTRL_POS = 0, 1, 2
@@ -28,7 +29,12 @@ class FgxConfig(ctypes.Structure):
         (n, ctypes.c_double) for n in (
             "dt", "duration", "tau", "delay", "alpha_phase", "bandwidth", "weights_scale",
             "goal_scale", "alpha", "pc_length", "p_gain", "d_gain", "act_low", "act_high",
-            "hole_width", "hole_depth", "hole_x", "collision_penalty")]
+            "hole_width", "hole_depth", "hole_x", "collision_penalty")] + [
+        (n, ctypes.c_int32) for n in (
+            "rew_fct", "learn_tau", "learn_delay", "learn_sub_trajectories")] + [
+        (n, ctypes.c_double) for n in (
+            "tau_bound_lo", "tau_bound_hi", "delay_bound_lo", "delay_bound_hi",
+            "via_x", "via_y", "target_x", "target_y")]
 
 
 class FgxDims(ctypes.Structure):

@@ -50,15 +50,14 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // ------------------------------------------------------------------------ dispatch
 // The episode kernels are instantiated per env kind in their own translation units
-// (fgx_ep_simple.hip, fgx_ep_hole.hip) so that the build compiles them in parallel.
+// (fgx_ep_simple.hip, fgx_ep_hole.hip, fgx_ep_via.hip) so that the build compiles them in parallel.
 #define FGX_FOR_NL(X) X(2) X(5)
 
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
-  const int rc = (h.dc.env == ENV_SIMPLE)
-                     ? fgx_launch_episode_simple(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err)
-                     : fgx_launch_episode_hole(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
-  return rc;
+  if (h.dc.env == ENV_SIMPLE) return fgx_launch_episode_simple(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
+  if (h.dc.env == ENV_HOLE) return fgx_launch_episode_hole(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
+  return fgx_launch_episode_via(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
 }
 
 static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, float* obs, hipStream_t stream) {
@@ -79,7 +78,14 @@ static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* m
 static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim) {
   if (c.abi_version != FGX_ABI_VERSION) return fail(FGX_E_INVALID, "abi_version mismatch");
   if (N <= 0) return fail(FGX_E_INVALID, "n_envs must be positive");
-  if (c.env_kind != FGX_ENV_SIMPLE && c.env_kind != FGX_ENV_HOLE) return fail(FGX_E_INVALID, "bad env_kind");
+  if (c.env_kind != FGX_ENV_SIMPLE && c.env_kind != FGX_ENV_HOLE && c.env_kind != FGX_ENV_VIA)
+    return fail(FGX_E_INVALID, "bad env_kind");
+  if (c.rew_fct < FGX_REW_SIMPLE || c.rew_fct > FGX_REW_UNBOUNDED) return fail(FGX_E_INVALID, "Unknown reward function");
+  if (c.rew_fct != FGX_REW_SIMPLE && c.env_kind != FGX_ENV_HOLE) return fail(FGX_E_INVALID, "rew_fct is a HoleReacher option");
+  if (c.learn_sub_trajectories && c.replan_period > 0)   // make_env_helpers.py:91-92
+    return fail(FGX_E_INVALID, "Cannot used sub-trajectory learning and replanning together.");
+  if (c.learn_tau || c.learn_delay || c.learn_sub_trajectories)
+    return fail(FGX_E_UNSUPPORTED, "learn_tau / learn_delay / learn_sub_trajectories not implemented yet");
   if (c.n_links < 1 || c.n_links > kMaxLinks) return fail(FGX_E_INVALID, "n_links out of range");
   if (c.mp_kind < FGX_MP_NONE || c.mp_kind > FGX_MP_PRODMP) return fail(FGX_E_INVALID, "bad mp_kind");
   if (c.ctrl_kind < FGX_CTRL_PD || c.ctrl_kind > FGX_CTRL_POS) return fail(FGX_E_INVALID, "bad ctrl_kind");
@@ -116,9 +122,10 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.time_aware = c.time_aware;
   d.return_context = c.return_context;
   const int n = c.n_links;
-  d.obs_dim = (c.env_kind == FGX_ENV_SIMPLE) ? 3 * n + 3 : 3 * n + 4;
+  d.obs_dim = (c.env_kind == FGX_ENV_SIMPLE) ? 3 * n + 3 : (c.env_kind == FGX_ENV_HOLE ? 3 * n + 4 : 3 * n + 5);
   d.full_dim = d.obs_dim + (c.time_aware ? 1 : 0);
-  // context mask (simple_reacher/mp_wrapper.py:32-40, hole_reacher/mp_wrapper.py:36-46)
+  // context mask (simple_reacher/mp_wrapper.py:32-40, hole_reacher/mp_wrapper.py:36-46,
+  // viapoint_reacher/mp_wrapper.py:27-35)
   int m = 0;
   for (int j = 0; j < 3 * n; ++j)
     if (c.random_start) d.ctx_idx[m++] = j;
@@ -126,6 +133,10 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   if (c.env_kind == FGX_ENV_HOLE) {
     if (std::isnan(c.hole_width)) d.ctx_idx[m++] = p;
     p += 1;
+  }
+  if (c.env_kind == FGX_ENV_VIA) {
+    if (std::isnan(c.via_x)) { d.ctx_idx[m++] = p; d.ctx_idx[m++] = p + 1; }
+    p += 2;
   }
   d.ctx_idx[m++] = p;
   d.ctx_idx[m++] = p + 1;
@@ -146,6 +157,14 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.rand_width = std::isnan(c.hole_width);
   d.rand_x = std::isnan(c.hole_x);
   d.rand_depth = std::isnan(c.hole_depth);
+  d.rew_fct = c.rew_fct;
+  if (c.env_kind == FGX_ENV_VIA && (std::isnan(c.via_x) != std::isnan(c.via_y) ||
+                                    std::isnan(c.target_x) != std::isnan(c.target_y)))
+    return fail(FGX_E_INVALID, "via_target / target must be given as (x, y) or left unset");
+  d.rand_via = std::isnan(c.via_x);
+  d.rand_target = std::isnan(c.target_x);
+  d.via_x0 = c.via_x; d.via_y0 = c.via_y;
+  d.tgt_x0 = c.target_x; d.tgt_y0 = c.target_y;
   d.n_split = (c.T > 128) ? ((c.T / 2) & ~7) : 0;
   d.dt = c.dt;
   d.tau = c.tau;
@@ -199,6 +218,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_qd = off; off = align_up(off + sizeof(double) * nl * N);
   const size_t o_goal = off; off = align_up(off + sizeof(double) * 2 * N);
   const size_t o_hole = off; off = align_up(off + sizeof(double) * 3 * N);
+  const size_t o_aux = off; off = align_up(off + sizeof(double) * 3 * N);
   const size_t o_steps = off; off = align_up(off + sizeof(int32_t) * N);
   const size_t o_plans = off; off = align_up(off + sizeof(int32_t) * N);
   const size_t o_flags = off; off = align_up(off + sizeof(uint32_t) * N);
@@ -213,6 +233,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.qd = (double*)(b + o_qd);
   h->st.goal = (double*)(b + o_goal);
   h->st.hole = (double*)(b + o_hole);
+  h->st.aux = (double*)(b + o_aux);
   h->st.steps = (int32_t*)(b + o_steps);
   h->st.plans = (int32_t*)(b + o_plans);
   h->st.flags = (uint32_t*)(b + o_flags);
@@ -360,8 +381,11 @@ int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward,
     if (h->dc.env == ENV_SIMPLE)                                                                               \
       hipLaunchKernelGGL((k_step_raw<ENV_SIMPLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions, \
                          obs, reward, terminated, truncated, final_obs, autoreset);                            \
-    else                                                                                                       \
+    else if (h->dc.env == ENV_HOLE)                                                                            \
       hipLaunchKernelGGL((k_step_raw<ENV_HOLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions,   \
+                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_step_raw<ENV_VIA, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions,    \
                          obs, reward, terminated, truncated, final_obs, autoreset);                            \
     HIP_TRY(hipGetLastError());                                                                                \
     return FGX_OK;                                                                                             \

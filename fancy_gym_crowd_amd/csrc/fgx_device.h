@@ -17,7 +17,8 @@ constexpr int kMaxLinks = 8;
 constexpr int kMaxObs = 3 * kMaxLinks + 5;
 constexpr int kMaxBasis = 16;
 
-enum : int { ENV_SIMPLE = 0, ENV_HOLE = 1 };
+enum : int { ENV_SIMPLE = 0, ENV_HOLE = 1, ENV_VIA = 2 };
+enum : int { REW_SIMPLE = 0, REW_VEL_ACC = 1, REW_UNBOUNDED = 2 };
 enum : int { MP_NONE = 0, MP_PROMP = 1, MP_DMP = 2, MP_PRODMP = 3, MP_GIVEN = 4 };
 enum : int { CTRL_PD = 0, CTRL_VEL = 1, CTRL_POS = 2 };
 
@@ -37,11 +38,14 @@ struct DevCfg {
   int out_dim;      // BB observation width (ctx_dim if return_context else full_dim)
   int n_params, rows, stride;
   int rand_width, rand_x, rand_depth;
+  int rew_fct;      // HoleReacher reward function (REW_*)
+  int rand_via, rand_target;   // ViaPointReacher: via point / target sampled at reset
   int n_split;      // numpy pairwise split point for a T-long return sum (0: none)
   int ctx_idx[kMaxObs + 1];
   double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;
   float act_lo32, act_hi32, dt32, rcp_dt32, tau32, rcp_tau32;
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
+  double via_x0, via_y0, tgt_x0, tgt_y0;
   float ws32, gs32, alpha32, beta32;
   double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
 };
@@ -51,10 +55,13 @@ struct DevState {
   double* q;       // [nl][N]
   double* qd;      // [nl][N]
   double* goal;    // [2][N]
-  double* hole;    // [3][N]  x, width, depth
+  double* hole;    // [3][N]  HoleReacher x, width, depth | ViaPointReacher via x, via y, -
+  double* aux;     // [3][N]  HoleReacher reward state: saved end effector x, y (unbounded),
+                   //         collision distance (vel_acc)
   int32_t* steps;  // [N] env steps since reset (== TimeLimit elapsed == current_traj_steps)
   int32_t* plans;  // [N] plan_steps (black_box_wrapper.py:88,199)
-  uint32_t* flags; // [N] bit0: qd holds an f32 array (velocity controller), bit1: has condition
+  uint32_t* flags; // [N] bit0: qd holds an f32 array (velocity controller), bit1: has condition,
+                   //     bit2: vel_acc reward function's sticky collision flag
   uint64_t* rng;   // [5][N]  state hi, state lo, inc hi, inc lo, (has_u32 << 32 | u32)
   float* cond;     // [2][nl][N] condition_on_desired pos / vel
   const float* tables;
@@ -187,7 +194,8 @@ template <int NL>
 struct Env {
   double q[NL], qd[NL];
   double gx, gy;
-  double hx, hw, hd;
+  double hx, hw, hd;     // HoleReacher hole | ViaPointReacher via point (hx, hw)
+  double ex, ey, cd;     // HoleReacher reward-function state (aux)
   int steps;
   uint32_t flags;
   // forward kinematics (base_reacher.py:95-103): joints[k+1] = cumsum of (cos, sin)(cumsum q)
@@ -250,26 +258,59 @@ struct Env {
     gx = x; gy = -d;
   }
 
+  // viapoint_reacher.py:56-77: via point in the disk of radius L/2, target in the annulus
+  // (L/2, L) by rejection (L = n_links, unit links); fixed values when configured
+  __device__ __forceinline__ void via_sample(const DevCfg& cf, Pcg64& r) {
+    const double total = (double)NL;
+    if (cf.rand_via) {
+      double v0 = total, v1 = total;
+      while (norm2(v0, v1) >= 0.5 * total) {
+        v0 = rng_uniform(r, -0.5 * total, 0.5 * total);
+        v1 = rng_uniform(r, -0.5 * total, 0.5 * total);
+      }
+      hx = v0; hw = v1;
+    } else {
+      hx = cf.via_x0; hw = cf.via_y0;
+    }
+    if (cf.rand_target) {
+      double g0 = total, g1 = total;
+      while (norm2(g0, g1) >= total || norm2(g0, g1) <= 0.5 * total) {
+        g0 = rng_uniform(r, -total, total);
+        g1 = rng_uniform(r, -total, total);
+      }
+      gx = g0; gy = g1;
+    } else {
+      gx = cf.tgt_x0; gy = cf.tgt_y0;
+    }
+    hd = 0.0;
+  }
+
   // seeded: reseed-only semantics (the discarded pre-seed goal draw has no effect);
   // unseeded: continue the stream exactly as the reference's reset() does.
+  // SimpleReacher and ViaPointReacher sample their goal(s), reset, sample again, reset again
+  // (simple_reacher.py:46-54, viapoint_reacher.py:46-54).
   __device__ __forceinline__ void reset(const DevCfg& cf, Pcg64& r, bool seeded, uint64_t seed) {
-    if (cf.env == ENV_SIMPLE) {
+    if (cf.env != ENV_HOLE) {
+      const bool via = (cf.env == ENV_VIA);
       if (seeded) {
         pcg_seed(r, seed);
         first_joint(cf, r);
-        goal_sample(r);
+        if (via) via_sample(cf, r); else goal_sample(r);
         pcg_seed(r, seed);
         first_joint(cf, r);
       } else {
-        goal_sample(r);
+        if (via) via_sample(cf, r); else goal_sample(r);
         first_joint(cf, r);
-        goal_sample(r);
+        if (via) via_sample(cf, r); else goal_sample(r);
         first_joint(cf, r);
       }
+      ex = ey = cd = 0.0;
     } else {
       if (seeded) pcg_seed(r, seed);
       hole_sample(cf, r);
       first_joint(cf, r);
+      cd = 0.0;   // reward_function.reset() (the saved end effector is rewritten before use)
+      ex = ey = 0.0;
     }
     fk();
   }

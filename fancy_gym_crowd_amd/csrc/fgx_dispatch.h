@@ -8,6 +8,9 @@
 int fgx_launch_episode_simple(const fgx::DevCfg& c, const fgx::DevState& s, int mp, const float* params,
                               const float* dpos, const float* dvel, const fgx::Outputs& o, hipStream_t stream,
                               std::string& err);
+int fgx_launch_episode_via(const fgx::DevCfg& c, const fgx::DevState& s, int mp, const float* params,
+                           const float* dpos, const float* dvel, const fgx::Outputs& o, hipStream_t stream,
+                           std::string& err);
 int fgx_launch_episode_hole(const fgx::DevCfg& c, const fgx::DevState& s, int mp, const float* params,
                             const float* dpos, const float* dvel, const fgx::Outputs& o, hipStream_t stream,
                             std::string& err);

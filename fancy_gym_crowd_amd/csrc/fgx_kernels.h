@@ -43,6 +43,10 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
     for (int k = 0; k < NL; ++k) put((float)v.qd[k]);
   }
   if (c.env == ENV_HOLE && (!ctx || c.rand_width)) put((float)v.hw);
+  if (c.env == ENV_VIA && (!ctx || c.rand_via)) {   // viapoint_reacher.py:116-126
+    put((float)(v.jx[NL] - v.hx));
+    put((float)(v.jy[NL] - v.hw));
+  }
   put((float)(v.jx[NL] - v.gx));
   put((float)(v.jy[NL] - v.gy));
   if (!ctx) {
@@ -59,6 +63,7 @@ __device__ __forceinline__ void load_env(const DevCfg& c, const DevState& s, int
   for (int k = 0; k < NL; ++k) { v.q[k] = s.q[k * N + e]; v.qd[k] = s.qd[k * N + e]; }
   v.gx = s.goal[e]; v.gy = s.goal[N + e];
   v.hx = s.hole[e]; v.hw = s.hole[N + e]; v.hd = s.hole[2 * N + e];
+  if (c.env == ENV_HOLE && c.rew_fct != REW_SIMPLE) { v.ex = s.aux[e]; v.ey = s.aux[N + e]; v.cd = s.aux[2 * N + e]; }
   v.steps = s.steps[e];
   v.flags = s.flags[e];
 }
@@ -70,6 +75,7 @@ __device__ __forceinline__ void store_env(const DevCfg& c, const DevState& s, in
   for (int k = 0; k < NL; ++k) { s.q[k * N + e] = v.q[k]; s.qd[k * N + e] = v.qd[k]; }
   s.goal[e] = v.gx; s.goal[N + e] = v.gy;
   s.hole[e] = v.hx; s.hole[N + e] = v.hw; s.hole[2 * N + e] = v.hd;
+  if (c.env == ENV_HOLE && c.rew_fct != REW_SIMPLE) { s.aux[e] = v.ex; s.aux[N + e] = v.ey; s.aux[2 * N + e] = v.cd; }
   s.steps[e] = v.steps;
   s.flags[e] = v.flags;
 }
@@ -205,8 +211,10 @@ struct Traj {
 // ============================================================================ env substep
 // One env.step with the (clipped) action a (f64) / a32 (when the action array is float32).
 // base_reacher_torque.py:20-37, base_reacher_direct.py:20-38, simple_reacher.py:56-70,
-// hole_reacher.py:255-259, hr_simple_reward.py:19-53.  Returns the reward; FK is refreshed
-// for HoleReacher always and for SimpleReacher only when the reward needs it or `fk_always`.
+// hole_reacher.py:255-259, hr_simple_reward.py:19-53, hr_dist_vel_acc_reward.py:20-60,
+// hr_unbounded_reward.py:17-59, viapoint_reacher.py:79-111.  Returns the reward; FK is
+// refreshed for the direct envs always and for SimpleReacher only when the reward needs it or
+// `fk_always`.
 struct StepOut {
   double reward, rdist, rctrl;
   bool coll, success;
@@ -243,22 +251,23 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
     if (MAYFK && st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
     r.reward = r.rdist - ctrl;
     r.rctrl = ctrl;
-  } else {
-    double acc_cost;
-    if (F32 && (v.flags & 1u)) {   // qd already holds a float32 array: f32 arithmetic
-      float s32 = 0.0f;
+  } else {   // direct velocity control: HoleReacher, ViaPointReacher
+    double acc_cost = 0.0;
+    if (ENV == ENV_HOLE) {   // ViaPointReacher's reward uses the action, not _acc
+      if (F32 && (v.flags & 1u)) {   // qd already holds a float32 array: f32 arithmetic
+        float s32 = 0.0f;
 #pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const float ac = div_rcp(a32[d] - (float)v.qd[d], c.dt32, c.rcp_dt32);
-        s32 = (d == 0) ? ac * ac : s32 + ac * ac;
-      }
-      acc_cost = (double)s32;
-    } else {
-      acc_cost = 0.0;
+        for (int d = 0; d < NL; ++d) {
+          const float ac = div_rcp(a32[d] - (float)v.qd[d], c.dt32, c.rcp_dt32);
+          s32 = (d == 0) ? ac * ac : s32 + ac * ac;
+        }
+        acc_cost = (double)s32;
+      } else {
 #pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double ac = div_rcp64(a[d] - v.qd[d], c.dt, c.rcp_dt);
-        acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
+        for (int d = 0; d < NL; ++d) {
+          const double ac = div_rcp64(a[d] - v.qd[d], c.dt, c.rcp_dt);
+          acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
+        }
       }
     }
 #pragma unroll
@@ -269,17 +278,77 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
     }
     if (F32) v.flags |= 1u;
     v.fk();
-    const bool sc = c.allow_self ? false : v.self_collision();
-    const bool wc = c.allow_wall ? false : v.wall_collision(c);
-    r.coll = sc || wc;
-    if (st == 199 || r.coll) {
-      const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
-      const double dc = dist * dist;
-      // np.dot([dist^2, acc, coll], [-1, -5e-8, -penalty]) == OpenBLAS forward fma chain
-      r.reward = __builtin_fma(r.coll ? 1.0 : 0.0, -c.penalty, __builtin_fma(acc_cost, -5e-8, dc * -1.0));
-      r.success = dist < 0.005 && !r.coll;
+    // sum(action**2) == sum(qd**2) after the step (f32 for a float32 action array)
+    double act_sq;
+    if (F32) {
+      float s32 = a32[0] * a32[0];
+#pragma unroll
+      for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
+      act_sq = (double)s32;
     } else {
-      r.reward = acc_cost * -5e-8;
+      act_sq = a[0] * a[0];
+#pragma unroll
+      for (int d = 1; d < NL; ++d) act_sq = act_sq + a[d] * a[d];
+    }
+    if (ENV == ENV_VIA) {   // viapoint_reacher.py:79-111
+      r.coll = c.allow_self ? false : v.self_collision();
+      // 5e-8 * np.sum(action**2): a float32 sum stays float32 (NEP 50)
+      const double pen_ctrl = F32 ? (double)(5e-8f * (float)act_sq) : 5e-8 * act_sq;
+      if (r.coll) {
+        const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+        r.reward = (-c.penalty - dist * dist) - pen_ctrl;
+      } else {   // reward starts at -inf and stays there (reference behaviour)
+        r.reward = -__builtin_inf();
+        if (st == 100) r.success = norm2(v.jx[NL] - v.hx, v.jy[NL] - v.hw) < 0.005;
+        else if (st == 199) r.success = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy) < 0.005;
+      }
+    } else if (c.rew_fct == REW_VEL_ACC) {   // hr_dist_vel_acc_reward.py:20-60
+      if (!(v.flags & 4u)) {
+        const bool sc = c.allow_self ? false : v.self_collision();
+        const bool wc = c.allow_wall ? false : v.wall_collision(c);
+        if (sc || wc) v.flags |= 4u;
+        v.cd = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+      }
+      r.coll = (v.flags & 4u) != 0;
+      double dist_cost = 0.0, coll_cost = 0.0;
+      if (st == 199) {
+        const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+        r.success = dist < 0.005 && !r.coll;
+        dist_cost = dist * dist;
+        coll_cost = r.coll ? v.cd * v.cd : 0.0;
+      }
+      // np.dot(features, (-1, -1e-4, -1e-6, -penalty, 0)): OpenBLAS forward fma chain
+      double d = dist_cost * -1.0;
+      d = __builtin_fma(act_sq, -1e-4, d);
+      d = __builtin_fma(acc_cost, -1e-6, d);
+      d = __builtin_fma(coll_cost, -c.penalty, d);
+      r.reward = __builtin_fma(0.0, 0.0, d);   // time_cost = 199 - steps is 0 whenever used
+    } else if (c.rew_fct == REW_UNBOUNDED) {   // hr_unbounded_reward.py:17-59
+      const bool sc = c.allow_self ? false : v.self_collision();
+      const bool wc = c.allow_wall ? false : v.wall_collision(c);
+      r.coll = sc || wc;
+      if (st == 180 || r.coll) { v.ex = v.jx[NL]; v.ey = v.jy[NL]; }
+      double dr = 0.0;
+      if (st == 199 || r.coll) {
+        const double dist = norm2(v.ex - v.gx, v.ey - v.gy);
+        if (r.coll) dr = 0.25 * exp(-dist);
+        else dr = (v.jy[NL] > 0.0) ? exp(-dist) : 1.0 - v.ey;
+        r.success = !r.coll;
+      }
+      r.reward = __builtin_fma(acc_cost, -5e-6, dr * 1.0);
+    } else {   // hr_simple_reward.py:19-53
+      const bool sc = c.allow_self ? false : v.self_collision();
+      const bool wc = c.allow_wall ? false : v.wall_collision(c);
+      r.coll = sc || wc;
+      if (st == 199 || r.coll) {
+        const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
+        const double dc = dist * dist;
+        // np.dot([dist^2, acc, coll], [-1, -5e-8, -penalty]) == OpenBLAS forward fma chain
+        r.reward = __builtin_fma(r.coll ? 1.0 : 0.0, -c.penalty, __builtin_fma(acc_cost, -5e-8, dc * -1.0));
+        r.success = dist < 0.005 && !r.coll;
+      } else {
+        r.reward = acc_cost * -5e-8;
+      }
     }
   }
   v.steps = st + 1;
@@ -378,7 +447,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
       ps.template add_fast<J, PH>(r.reward);
       return false;
     } else {
-      term = (ENV == ENV_HOLE) ? r.coll : false;
+      term = (ENV != ENV_SIMPLE) ? r.coll : false;
       trunc = v.steps >= c.max_steps;
       ps.add(k, r.reward, split);
     }
@@ -391,7 +460,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
       if (o.step_rewards) o.step_rewards[ek] = r.reward;
       if (o.step_obs) emit_obs(c, v, false, o.step_obs + ek * c.full_dim, nullptr);
-      if (ENV == ENV_HOLE) {
+      if (ENV != ENV_SIMPLE) {
         if (o.is_collided) { o.is_collided[ek] = r.coll; o.is_success[ek] = r.success; }
         if (o.end_effector) { o.end_effector[ek * 2] = v.jx[NL]; o.end_effector[ek * 2 + 1] = v.jy[NL]; }
       } else if (o.reward_dist) {
@@ -499,7 +568,7 @@ __global__ __launch_bounds__(256) void k_step_raw(DevCfg c, DevState s, const fl
 #pragma unroll
   for (int d = 0; d < NL; ++d) { a32[d] = act[e * NL + d]; a[d] = (double)a32[d]; }
   const StepOut r = substep<ENV, true, NL>(c, v, a, a32, true);
-  const bool te = (ENV == ENV_HOLE) && r.coll, tr = v.steps >= c.max_steps;
+  const bool te = (ENV != ENV_SIMPLE) && r.coll, tr = v.steps >= c.max_steps;
   rew[e] = r.reward;
   term[e] = te;
   trunc[e] = tr;

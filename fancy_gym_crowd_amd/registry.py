@@ -6,8 +6,9 @@ Mirrors (paths relative to /root/reference/fancy_gym):
   register / upgrade           envs/registry.py:137-220   ('{ns}_{MP}/{name}' ids, registry.py:243)
   bb_env_constructor           envs/registry.py:280-309   (defaults <- MPWrapper.mp_config <- overrides)
   make_bb                      utils/make_env_helpers.py:68-136 (duration, tau, TimeAwareObservation)
-  reacher registrations        envs/__init__.py:57-65, 658-666, 682-698
-  MPWrapper.mp_config          simple_reacher/mp_wrapper.py:10-30, hole_reacher/mp_wrapper.py:10-32
+  reacher registrations        envs/__init__.py:57-65, 658-666, 669-679, 682-698
+  MPWrapper.mp_config          simple_reacher/mp_wrapper.py:10-30, hole_reacher/mp_wrapper.py:10-32,
+                               viapoint_reacher/mp_wrapper.py:10-25
 Third-party defaults restated from mp_pytorch<=0.1.3 [EXT-M] (not in the container).
 """
 import copy
@@ -59,7 +60,7 @@ class EnvSpec:
 
     def __init__(self, id, kind, kwargs, max_episode_steps, mp_config):
         self.id = id
-        self.kind = kind                      # 'simple' (torque) | 'hole' (direct velocity)
+        self.kind = kind                      # 'simple' (torque) | 'hole' | 'via' (direct velocity)
         self.kwargs = dict(kwargs)
         self.max_episode_steps = max_episode_steps
         self.mp_config = mp_config
@@ -78,6 +79,14 @@ _HOLE_MP_CONFIG = {     # hole_reacher/mp_wrapper.py:10-32
     'DMP': {'controller_kwargs': {'controller_type': 'velocity'},
             'trajectory_generator_kwargs': {'weights_scale': 500},
             'phase_generator_kwargs': {'alpha_phase': 2.5}},
+    'ProDMP': {},
+}
+
+_VIA_MP_CONFIG = {      # viapoint_reacher/mp_wrapper.py:10-25
+    'ProMP': {'controller_kwargs': {'controller_type': 'velocity'}},
+    'DMP': {'controller_kwargs': {'controller_type': 'velocity'},
+            'trajectory_generator_kwargs': {'weights_scale': 50},
+            'phase_generator_kwargs': {'alpha_phase': 2}},
     'ProDMP': {},
 }
 
@@ -138,6 +147,8 @@ register('fancy/HoleReacher-v0', 'hole', {'n_links': 5, 'random_start': True, 'a
                                           'allow_wall_collision': False, 'hole_width': None,
                                           'hole_depth': 1, 'hole_x': None, 'collision_penalty': 100},
          200, _HOLE_MP_CONFIG)
+register('fancy/ViaPointReacher-v0', 'via', {'n_links': 5, 'allow_self_collision': False, 'collision_penalty': 1000},
+         200, _VIA_MP_CONFIG)
 
 
 # --------------------------------------------------------------------------- replanning schedules
@@ -199,24 +210,40 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c.abi_version = _lib.FGX_ABI_VERSION
     n = int(kw['n_links'])
     c.n_links = n
-    c.env_kind = _lib.ENV_SIMPLE if spec.kind == 'simple' else _lib.ENV_HOLE
-    rs_default = True if spec.kind == 'simple' else False     # HoleReacherEnv default random_start=False
+    c.env_kind = {'simple': _lib.ENV_SIMPLE, 'hole': _lib.ENV_HOLE, 'via': _lib.ENV_VIA}[spec.kind]
+    # constructor defaults: SimpleReacherEnv random_start=True; HoleReacherEnv / ViaPointReacherEnv False
+    rs_default = spec.kind == 'simple'
     c.random_start = int(bool(kw.get('random_start', rs_default)))
     c.allow_self_collision = int(bool(kw.get('allow_self_collision', False)))
     c.allow_wall_collision = int(bool(kw.get('allow_wall_collision', False)))
     c.dt = 0.01                                                # base_reacher.py:21
     c.max_episode_steps = int(spec.max_episode_steps)
     nan = float('nan')
+    c.hole_width = c.hole_depth = c.hole_x = nan
+    c.via_x = c.via_y = c.target_x = c.target_y = nan
+    c.rew_fct = _lib.REW_SIMPLE
     if spec.kind == 'hole':
         c.hole_width = nan if kw.get('hole_width', 1.0) is None else float(kw.get('hole_width', 1.0))
         c.hole_depth = nan if kw.get('hole_depth') is None else float(kw['hole_depth'])
         c.hole_x = nan if kw.get('hole_x') is None else float(kw['hole_x'])
         c.collision_penalty = float(kw.get('collision_penalty', 1000))
         bound = float(np.float32(2 * np.pi))                   # Box(float32) bounds, base_reacher_direct.py:16-18
-        if kw.get('rew_fct', 'simple') != 'simple':
-            raise NotImplementedError("HoleReacher rew_fct other than 'simple' (hr_simple_reward.py)")
+        rew = kw.get('rew_fct', 'simple')                      # hole_reacher.py:48-58
+        if rew not in ('simple', 'vel_acc', 'unbounded'):
+            raise ValueError("Unknown reward function {}".format(rew))
+        c.rew_fct = {'simple': _lib.REW_SIMPLE, 'vel_acc': _lib.REW_VEL_ACC, 'unbounded': _lib.REW_UNBOUNDED}[rew]
+    elif spec.kind == 'via':
+        c.collision_penalty = float(kw.get('collision_penalty', 1000))
+        bound = float(np.float32(2 * np.pi))
+        for key, (fx, fy) in (('via_target', ('via_x', 'via_y')), ('target', ('target_x', 'target_y'))):
+            v = kw.get(key)
+            if v is not None:
+                v = np.asarray(v, dtype=np.float64).reshape(-1)
+                if v.shape != (2,):
+                    raise ValueError(f"{key} must be an (x, y) pair")
+                setattr(c, fx, float(v[0]))
+                setattr(c, fy, float(v[1]))
     else:
-        c.hole_width = c.hole_depth = c.hole_x = nan
         bound = 1000.0                                          # base_reacher_torque.py:16-18
         if kw.get('target') is not None:
             raise NotImplementedError("SimpleReacher with a fixed target")

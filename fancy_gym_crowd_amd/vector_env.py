@@ -106,16 +106,18 @@ class BlackBoxVectorEnv:
 
     def _obs_space(self, cfg):
         n = self.dof
-        if cfg.env_kind == _lib.ENV_SIMPLE:
-            bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf] * 2, [np.inf]])
-        else:
-            bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf], [np.inf] * 2, [np.inf]])
+        extra = {_lib.ENV_SIMPLE: 0, _lib.ENV_HOLE: 1, _lib.ENV_VIA: 2}[cfg.env_kind]   # width | via - ee
+        bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf] * extra, [np.inf] * 2, [np.inf]])
         low, high = -bound, bound
         if cfg.time_aware:
             low, high = np.append(low, 0.0), np.append(high, 1.0)
         if cfg.return_context:
             rs = [bool(cfg.random_start)] * (3 * n)
-            mask = rs + ([math_isnan(cfg.hole_width)] if cfg.env_kind == _lib.ENV_HOLE else []) + [True, True, False]
+            if cfg.env_kind == _lib.ENV_HOLE:
+                rs = rs + [math_isnan(cfg.hole_width)]
+            elif cfg.env_kind == _lib.ENV_VIA:
+                rs = rs + [math_isnan(cfg.via_x)] * 2
+            mask = rs + [True, True, False]
             low, high = low[np.array(mask)], high[np.array(mask)]
         return Box(low, high, dtype=np.float32)
 
@@ -158,7 +160,7 @@ class BlackBoxVectorEnv:
         info.positions, info.velocities = b["positions"].data_ptr(), b["velocities"].data_ptr()
         info.step_actions, info.step_obs = b["step_actions"].data_ptr(), b["step_observations"].data_ptr()
         info.step_rewards = b["step_rewards"].data_ptr()
-        if self.meta["kind"] == "hole":
+        if self.meta["kind"] in ("hole", "via"):
             b["is_collided"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
             b["is_success"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
             b["end_effector"] = torch.full((N, T, 2), float("nan"), dtype=torch.float64, device=dev)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 1
+#define FGX_ABI_VERSION 2
 
 /* error codes */
 #define FGX_OK 0
@@ -54,9 +54,16 @@ extern "C" {
 #define FGX_E_NOMEM (-3)     /* device allocation failed                                     */
 #define FGX_E_UNSUPPORTED (-4) /* configuration outside what the engine implements           */
 
-/* env kinds (reference: SimpleReacherEnv = torque, HoleReacherEnv = direct velocity) */
+/* env kinds (reference: SimpleReacherEnv = torque; HoleReacherEnv, ViaPointReacherEnv = direct
+ * velocity; envs/__init__.py:56-698) */
 #define FGX_ENV_SIMPLE 0
 #define FGX_ENV_HOLE 1
+#define FGX_ENV_VIA 2
+
+/* HoleReacher reward functions (hole_reacher.py:48-58, rew_fct) */
+#define FGX_REW_SIMPLE 0     /* hr_simple_reward.py        */
+#define FGX_REW_VEL_ACC 1    /* hr_dist_vel_acc_reward.py  */
+#define FGX_REW_UNBOUNDED 2  /* hr_unbounded_reward.py     */
 
 /* trajectory generators (reference: trajectory_generator_factory.py:7-21) */
 #define FGX_MP_NONE 0   /* step-based env only (fgx_step_raw)                */
@@ -104,7 +111,16 @@ typedef struct fgx_config {
   double p_gain, d_gain;        /* PD gains                                                 */
   double act_low, act_high;     /* env action-space bounds as stored by gymnasium Box (f32) */
   double hole_width, hole_depth, hole_x; /* NaN = sampled at reset (hole_reacher.py:261-294) */
-  double collision_penalty;     /* HoleReacher reward (hr_simple_reward.py:14)              */
+  double collision_penalty;     /* HoleReacher / ViaPointReacher reward                     */
+  /* ---- ABI 2 */
+  int32_t rew_fct;              /* FGX_REW_* (HoleReacher only)                             */
+  int32_t learn_tau;            /* phase_generator_kwargs learn_tau: params = [tau, ...]    */
+  int32_t learn_delay;          /* learn_delay: params = [(tau,) delay, ...]                */
+  int32_t learn_sub_trajectories; /* black_box_kwargs (black_box_wrapper.py:106-113)        */
+  double tau_bound_lo, tau_bound_hi;     /* make_env_helpers.py:118-122 ([2 dt, duration])  */
+  double delay_bound_lo, delay_bound_hi; /* make_env_helpers.py:124-126 ([0, duration-2dt]) */
+  double via_x, via_y;          /* ViaPointReacher via_target (NaN = sampled, viapoint_reacher.py:60-66) */
+  double target_x, target_y;    /* ViaPointReacher target     (NaN = sampled, :68-74)      */
 } fgx_config;
 
 typedef struct fgx_dims {
@@ -166,7 +182,8 @@ int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward,
                  void* stream);
 
 /* State access (tests / checkpoint): q, qd [N, dof] f64, goal [N, 2] f64, hole [N, 3] f64
- * (x, width, depth), steps [N] i32.  Any pointer may be NULL. */
+ * (HoleReacher: x, width, depth; ViaPointReacher: via x, via y, 0), steps [N] i32.
+ * Any pointer may be NULL. */
 int fgx_get_state(void* handle, double* q, double* qd, double* goal, double* hole, int32_t* steps,
                   void* stream);
 int fgx_set_state(void* handle, const double* q, const double* qd, const double* goal,

@@ -53,17 +53,17 @@ def test_library_loads_and_reports_abi():
 
 
 def test_config_struct_layout_matches_header():
-    # 20 int32 then 18 doubles (see include/fgx.h)
-    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8
+    # 20 int32, 18 doubles, then (ABI 2) 4 int32 and 8 doubles (see include/fgx.h)
+    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8
     assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
 
 
 def test_registry_ids():
     # registry.py:243 -> '{ns}_{mp}/{name}'
     for mp in fgx.KNOWN_MPS:
-        for name in ("SimpleReacher-v0", "LongSimpleReacher-v0", "HoleReacher-v0"):
+        for name in ("SimpleReacher-v0", "LongSimpleReacher-v0", "HoleReacher-v0", "ViaPointReacher-v0"):
             assert f"fancy_{mp}/{name}" in fgx.ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS[mp]
-    assert len(fgx.ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS["all"]) == 9
+    assert len(fgx.ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS["all"]) == 12
     assert fgx.MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS["fancy"]["ProDMP"]
 
 
@@ -83,6 +83,9 @@ def test_nested_update_type_key_replaces():
     ("ProMP", "HoleReacher-v0", 25, _lib.CTRL_VEL, None, None),
     ("DMP", "HoleReacher-v0", 30, _lib.CTRL_VEL, None, None),
     ("ProDMP", "HoleReacher-v0", 30, _lib.CTRL_PD, 1.0, 0.1),
+    ("ProMP", "ViaPointReacher-v0", 25, _lib.CTRL_VEL, None, None),
+    ("DMP", "ViaPointReacher-v0", 30, _lib.CTRL_VEL, None, None),
+    ("ProDMP", "ViaPointReacher-v0", 30, _lib.CTRL_PD, 1.0, 0.1),
 ])
 def test_resolved_configs(mp, name, n_params, ctrl, p, d):
     c, meta = fgx.resolve(f"fancy_{mp}/{name}")
@@ -93,8 +96,8 @@ def test_resolved_configs(mp, name, n_params, ctrl, p, d):
     assert c.T == 200 and c.duration == 2.0                     # make_env_helpers.py:110-113
     assert c.tau == (1.5 if mp == "ProDMP" else 2.0)
     if mp == "DMP":
-        assert c.weights_scale == (50 if "Simple" in name else 500)
-        assert c.alpha_phase == (2 if "Simple" in name else 2.5)
+        assert c.weights_scale == (500 if "Hole" in name else 50)
+        assert c.alpha_phase == (2.5 if "Hole" in name else 2)
     if mp == "ProMP":
         assert c.zero_start == 1 and c.n_basis == 5
         assert c.weights_scale == (2 if "Hole" in name else 1)
@@ -102,6 +105,18 @@ def test_resolved_configs(mp, name, n_params, ctrl, p, d):
         assert c.act_high == float(np.float32(2 * np.pi))       # Box(float32) bound
         assert np.isnan(c.hole_width) and np.isnan(c.hole_x) and c.hole_depth == 1.0
         assert c.collision_penalty == 100
+    if "ViaPoint" in name:   # envs/__init__.py:669-679, viapoint_reacher.py:15-16
+        assert c.env_kind == _lib.ENV_VIA and c.random_start == 0 and c.collision_penalty == 1000
+        assert np.isnan(c.via_x) and np.isnan(c.target_x)
+
+
+def test_hole_reward_function_option():
+    c, _ = fgx.resolve("fancy_ProMP/HoleReacher-v0", rew_fct="vel_acc")
+    assert c.rew_fct == _lib.REW_VEL_ACC
+    c, _ = fgx.resolve("fancy_ProMP/HoleReacher-v0", rew_fct="unbounded")
+    assert c.rew_fct == _lib.REW_UNBOUNDED
+    with pytest.raises(ValueError):   # hole_reacher.py:57-58
+        fgx.resolve("fancy_ProMP/HoleReacher-v0", rew_fct="foo")
 
 
 def test_replanning_schedule_compiles_to_period():
@@ -135,3 +150,6 @@ def test_context_space_sizes():
         n = c.n_links
         full = 3 * n + 3 if "Simple" in name else 3 * n + 4
         assert ctx == full - 1
+    # ViaPointReacher (random_start False): via - ee and goal - ee only
+    from oracle import port
+    assert int(port.Reacher("ViaPointReacher").context_mask().sum()) == 4
