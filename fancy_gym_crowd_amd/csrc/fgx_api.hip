@@ -165,7 +165,6 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.rand_target = std::isnan(c.target_x);
   d.via_x0 = c.via_x; d.via_y0 = c.via_y;
   d.tgt_x0 = c.target_x; d.tgt_y0 = c.target_y;
-  d.n_split = (c.T > 128) ? ((c.T / 2) & ~7) : 0;
   d.dt = c.dt;
   d.tau = c.tau;
   d.p_gain = c.p_gain;
@@ -226,6 +225,9 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_cond = off; off = align_up(off + sizeof(float) * 2 * nl * N);
   const size_t o_seed = off; off = align_up(off + sizeof(uint64_t) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
+  // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128)
+  const bool need_rew = cfg->env_kind != FGX_ENV_SIMPLE && cfg->mp_kind != FGX_MP_NONE && h->dc.T > 128;
+  const size_t o_rew = off; off = align_up(off + (need_rew ? sizeof(double) * (size_t)h->dc.T * N : 0));
   e = hipMalloc(&h->state_block, off);
   if (e != hipSuccess) { delete h; return fail(FGX_E_NOMEM, std::string("hipMalloc state: ") + hipGetErrorString(e)); }
   char* b = (char*)h->state_block;
@@ -240,6 +242,8 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.rng = (uint64_t*)(b + o_rng);
   h->st.cond = (float*)(b + o_cond);
   h->tables = (float*)(b + o_tab);
+  h->st.rew = need_rew ? (double*)(b + o_rew) : nullptr;
+  h->st.plan_len = nullptr;
   h->st.tables = h->tables;
   (void)hipMemset(h->state_block, 0, off);
   // basis tables

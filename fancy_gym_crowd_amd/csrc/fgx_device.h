@@ -40,7 +40,6 @@ struct DevCfg {
   int rand_width, rand_x, rand_depth;
   int rew_fct;      // HoleReacher reward function (REW_*)
   int rand_via, rand_target;   // ViaPointReacher: via point / target sampled at reset
-  int n_split;      // numpy pairwise split point for a T-long return sum (0: none)
   int ctx_idx[kMaxObs + 1];
   double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;
   float act_lo32, act_hi32, dt32, rcp_dt32, tau32, rcp_tau32;
@@ -64,6 +63,9 @@ struct DevState {
                    //     bit2: vel_acc reward function's sticky collision flag
   uint64_t* rng;   // [5][N]  state hi, state lo, inc hi, inc lo, (has_u32 << 32 | u32)
   float* cond;     // [2][nl][N] condition_on_desired pos / vel
+  double* rew;     // [T][N] step rewards of the current BB step (direct envs with T > 128 only):
+                   //        the exact numpy pairwise return for lengths 128 < L <= T
+  const int32_t* plan_len;   // [N] per-env plan length (learned tau / sub-trajectories) or null
   const float* tables;
 };
 
@@ -128,8 +130,8 @@ __device__ __forceinline__ bool ccw(double ax, double ay, double bx, double by, 
   return (cy - ay) * (bx - ax) - (by - ay) * (cx - ax) > 1e-12;   // classic_control/utils.py:1-2
 }
 
-// numpy pairwise summation (np.sum of a length-L f64 vector, L <= 256) done online.
-// Exact for L <= 128 and for L in [2*split .. split + 128] with split = (Tcap/2) & ~7.
+// numpy pairwise summation (np.sum of a length-L f64 vector, L <= 256) done online: exact for
+// L <= 128, and for 128 < L <= 256 when split == (L/2) & ~7 (the caller knows L in advance).
 struct PairwiseSum {
   double a[8], t;       // single-level state (valid for L <= 128)
   double b[8], u;       // second-half state (t >= split)
@@ -169,6 +171,31 @@ struct PairwiseSum {
     return first + u;
   }
 };
+
+// numpy pairwise_sum (umath loops_utils.h) over a[0], a[st], ..., a[(n-1) st], n <= 256
+__device__ inline double pairwise_strided(const double* a, int64_t st, int n) {
+  auto block = [&](int lo, int m) -> double {
+    if (m < 8) {
+      double r = 0.0;
+      for (int i = 0; i < m; ++i) r = r + a[(lo + i) * st];
+      return r;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[(lo + j) * st];
+    int i = 8;
+    for (; i < m - (m % 8); i += 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + a[(lo + i + j) * st];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < m; ++i) res = res + a[(lo + i) * st];
+    return res;
+  };
+  if (n <= 128) return block(0, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return block(0, n2) + block(n2, n - n2);
+}
 
 // ------------------------------------------------------------------ RNG state load/store
 __device__ __forceinline__ Pcg64 load_rng(const uint64_t* rng, int64_t N, int64_t e) {

@@ -393,7 +393,18 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
                            ? (c.replan - 1 - (s0 % c.replan)) : -1;
   PairwiseSum ps;
   ps.init();
-  const int split = c.n_split;
+  // plan length and the numpy pairwise split point of the return sum.  SimpleReacher never
+  // terminates, so its episode-segment length is known now (plan end, TimeLimit or the
+  // replanning sample) and the two-level online sum is exact; the direct envs can stop at any
+  // sample (collision) and keep their step rewards in s.rew for lengths above 128.
+  const int Te = (MP == MP_GIVEN && s.plan_len) ? s.plan_len[e] : c.T;
+  int split = 0;
+  if (ENV == ENV_SIMPLE) {
+    int Lp = min(Te, max(1, c.max_steps - v.steps));
+    if (k_replan >= 0) Lp = min(Lp, k_replan + 1);
+    split = (Lp > 128) ? ((Lp / 2) & ~7) : 0;
+  }
+  double* rew_row = (ENV != ENV_SIMPLE && s.rew) ? s.rew + e : nullptr;
   bool term = false, trunc = false, stop = false;
   float pos[NL], vel[NL];
   constexpr bool F32 = (CTRL != CTRL_PD);
@@ -450,6 +461,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
       term = (ENV != ENV_SIMPLE) ? r.coll : false;
       trunc = v.steps >= c.max_steps;
       ps.add(k, r.reward, split);
+      if (ENV != ENV_SIMPLE && rew_row) rew_row[(int64_t)k * N] = r.reward;
     }
     // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
     if (LOG) {
@@ -488,15 +500,17 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // the blocks carry no per-lane control flow; the wave runs the blocks every lane can take.
     int lim = min(199, c.max_steps - 1) - v.steps;
     if (k_replan >= 0) lim = min(lim, k_replan);
-    int nfast = min(c.T, max(0, lim)) / 8;
+    int nfast = min(Te, max(0, lim)) / 8;
     if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
+    const int usplit = __builtin_amdgcn_readfirstlane(split);
+    if (__ballot(split != usplit) != 0) nfast = 0;   // the block phases need one split per wave
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nfast = min(nfast, __shfl_xor(nfast, off, 64));
     nfast = __builtin_amdgcn_readfirstlane(nfast);
     for (int kb = 0; kb < 8 * nfast; kb += 8) {
-      if (split > 0 && kb == split) ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
+      if (usplit > 0 && kb == usplit) ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
       // phase of this block (uniform): pushes into the level-1 and/or second-half sums
-      const int ph = (kb < 128 ? 1 : 0) | ((split > 0 && kb >= split) ? 2 : 0);
+      const int ph = (kb < 128 ? 1 : 0) | ((usplit > 0 && kb >= usplit) ? 2 : 0);
 #define FGX_SAMPLE(J, PH) sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}, false);
 #define FGX_BLOCK(PH) \
       FGX_SAMPLE(0, PH) FGX_SAMPLE(1, PH) FGX_SAMPLE(2, PH) FGX_SAMPLE(3, PH) \
@@ -507,12 +521,11 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
     k = 8 * nfast;
   }
-  while (!stop && k < c.T) {
+  while (!stop && k < Te) {
     stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG);
     ++k;
   }
-  k -= 1;   // index of the last executed sample
-  const int L = (k < c.T) ? k + 1 : c.T;
+  const int L = k;   // samples executed (trajectory_length)
   // the full desired plan is reported (black_box_wrapper.py:245-246)
   if (LOG && o.positions && MP != MP_GIVEN) {
     for (int kk = L; kk < c.T; ++kk) {
@@ -522,7 +535,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
   }
   if (ENV == ENV_SIMPLE && !LOG) v.fk();
-  o.ret[e] = ps.result(L, split);
+  o.ret[e] = (ENV != ENV_SIMPLE && L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
   o.term[e] = term;
   o.trunc[e] = trunc;
   o.tlen[e] = L;

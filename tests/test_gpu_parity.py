@@ -73,6 +73,17 @@ def split_tables(spec, arr):
     return dict(psi=arr[:, :nb], sdt=arr[:, nb])
 
 
+def assert_ulps(got, ref, max_ulps):
+    """f64 arrays equal within max_ulps units in the last place (infinities must match)."""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    fin = np.isfinite(ref)
+    np.testing.assert_array_equal(got[~fin], ref[~fin])
+    ulps = np.abs(got[fin] - ref[fin]) / np.spacing(np.abs(ref[fin]))
+    bad = np.nonzero(ulps > max_ulps)[0]
+    assert bad.size == 0, (f"{bad.size} values beyond {max_ulps} ulp (max {ulps.max():.1f}): "
+                           f"got={got[fin][bad][:4]}, ref={ref[fin][bad][:4]}")
+
+
 def ulp_diff32(a, b):
     a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
     b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
@@ -232,17 +243,10 @@ def test_bb_step_vs_oracle(ci):
         np.testing.assert_array_equal(np_(info["positions"]), r_info["positions"])
         np.testing.assert_array_equal(np_(info["velocities"]), r_info["velocities"])
         close(np_(ret), r_ret)
-        # numpy's pairwise order is reproduced exactly for L <= 128 and L >= 192 (T = 200);
-        # other lengths (HoleReacher collisions in (128, 192)) agree to rounding only
-        L_ = r_info["trajectory_length"]
-        exact_ok = (L_ <= 128) | (L_ >= 192)
+        # numpy's pairwise summation order is reproduced for every trajectory length
         # (np.linalg.norm / np.dot go through the host BLAS: the kernel follows the OpenBLAS
         # fma ordering pinned by the goldens; another host BLAS may round differently by an ulp)
-        g_, r_ = np_(ret)[exact_ok], r_ret[exact_ok]
-        ulps = np.abs(g_ - r_) / np.spacing(np.abs(r_))
-        bad = np.nonzero(ulps > 16)[0]
-        assert bad.size == 0, (f"returns beyond 16 ulp: {bad.size} envs, max {ulps.max():.1f} ulp, "
-                               f"L={L_[exact_ok][bad][:8]}, got={g_[bad][:4]}, ref={r_[bad][:4]}")
+        assert_ulps(np_(ret), r_ret, 16)
         n_exact += int((np_(ret) == r_ret).sum())
         close(np_(info["final_observation"]), r_info["final_obs"])
         close(np_(obs), r_obs)
@@ -269,6 +273,9 @@ def test_bb_step_vs_oracle(ci):
 FAST = FULL + [
     ("fancy_DMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}}, 256, 8),
     ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(64)}}, 192, 6),
+    # segment lengths 150 / 50 and 170 / 30: the pairwise split (L/2) & ~7 != that of T = 200
+    ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(150)}}, 128, 4),
+    ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(170)}}, 128, 4),
 ]
 
 
@@ -295,6 +302,7 @@ def test_bb_fast_path_vs_oracle(ci):
         np.testing.assert_array_equal(np_(te), r_te)
         np.testing.assert_array_equal(np_(tr), r_tr)
         close(np_(ret), r_ret)
+        assert_ulps(np_(ret), r_ret, 16)
         n_exact += int((np_(ret) == r_ret).sum())
         close(np_(info["final_observation"]), r_info["final_obs"])
         close(np_(obs), r_obs)
