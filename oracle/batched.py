@@ -290,17 +290,24 @@ class BatchedBB:
 
     def __init__(self, name, N, ctrl, mp_spec=None, traj_fn=None, replan_period=0,
                  max_planning_times=np.inf, condition_on_desired=False, info_level=0,
-                 time_aware=None, tables=None, env_kwargs=None):
+                 time_aware=None, tables=None, env_kwargs=None, learned=None):
         self.env = BatchedReacher(name, N, **(env_kwargs or {}))
         self.N = N
         self.ctrl = ctrl
         self.spec = mp_spec
         self.replan = replan_period
-        self.time_aware = (replan_period > 0) if time_aware is None else time_aware
-        self.return_context = replan_period == 0
+        sub = bool(learned and learned.get("sub_traj"))
+        self.time_aware = (replan_period > 0 or sub) if time_aware is None else time_aware
+        self.return_context = replan_period == 0 and not sub
         self.max_planning_times = max_planning_times
         self.condition_on_desired = condition_on_desired
         self.info_level = info_level
+        if learned is not None:   # per-env tau / delay (make_env_helpers.py:115-126)
+            lk = dict(learned)
+            traj_fn = lambda params, s0, q, qd: mpm.trajectory_learned(
+                mp_spec, params, s0, q, qd, learn_tau=lk.get("learn_tau", False) or sub,
+                learn_delay=lk.get("learn_delay", False), sub_traj=sub,
+                tau_bound=lk.get("tau_bound"), delay_bound=lk.get("delay_bound"))
         if traj_fn is None:
             self.T = mp_spec.T
             self.tables = tables if tables is not None else mpm.build_tables(
@@ -343,8 +350,10 @@ class BatchedBB:
             q_c[self.has_cond] = self.cond_pos[self.has_cond]
             qd_c[self.has_cond] = self.cond_vel[self.has_cond]
         s0 = self.traj_steps if self.replan > 0 else np.zeros(N, np.int64)
-        pos, vel = self.traj_fn(params, s0, q_c, qd_c)
+        out = self.traj_fn(params, s0, q_c, qd_c)
+        pos, vel = out[0], out[1]
         T = pos.shape[1]
+        plan_len = out[2] if len(out) > 2 else np.full(N, T)
         act = np.ones(N, bool)
         rewards = np.zeros((N, T))
         tlen = np.zeros(N, np.int64)
@@ -383,7 +392,7 @@ class BatchedBB:
             replan_now = np.zeros(N, bool)
             if self.replan > 0:
                 replan_now = ((t + 1 + self.traj_steps) % self.replan == 0) & (self.plan_steps < self.max_planning_times)
-            stop = act & (te | tr | replan_now)
+            stop = act & (te | tr | replan_now | (t + 1 >= plan_len))
             if self.condition_on_desired and np.any(stop):
                 if self.cond_pos is None:
                     self.cond_pos = np.zeros((N, n), f32)

@@ -34,7 +34,7 @@ ProDMP      q(s) = c1 y1(s) + c2 y2(s) + Phi_p(s).[w; g], y1 = exp(-alpha s/2), 
             rounded grid index; (c1, c2) solved from q(s0) = q0, q'(s0) = tau*qd0 (2x2
             Wronskian).  params = per-dof blocks [w_d (n_b), g_d] (num_basis_g = n_b + 1).
 """
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 
 import numpy as np
 
@@ -62,10 +62,11 @@ class MPSpec:
     dt: float = 0.01
     duration: float = 2.0
     extra: dict = field(default_factory=dict)
+    T_override: int = 0            # learn_sub_trajectories: T = round(tau / dt) per env
 
     @property
     def T(self):
-        return int(round(self.duration / self.dt))
+        return self.T_override or int(round(self.duration / self.dt))
 
     @property
     def n_params(self):
@@ -238,3 +239,56 @@ def trajectory(spec, tables, params, s0, q0, qd0):
         vel = (fma_chain32(Hv[:, :, None, :], coef[:, None, :, :]) / tau32).astype(f32)
         return pos, vel
     raise ValueError(spec.kind)
+
+
+# ----------------------------------------------------------------------------- learned tau / delay
+def learned_params(spec, params, learn_tau, learn_delay, tau_bound, delay_bound):
+    """Split params [tau?, delay?, w...] after BlackBoxWrapper.get_trajectory's clip to the
+    float32 action-space bounds (black_box_wrapper.py:115-119; bounds from
+    make_env_helpers.py:118-126 via the phase generator's tau_bound / delay_bound)."""
+    p = np.asarray(params, f32)
+    p = p.reshape(p.shape[0], -1)
+    lo = np.full(p.shape[1], -np.inf, f32)
+    hi = np.full(p.shape[1], np.inf, f32)
+    i = 0
+    if learn_tau:
+        lo[0], hi[0] = f32(tau_bound[0]), f32(tau_bound[1])
+        i = 1
+    if learn_delay:
+        lo[i], hi[i] = f32(delay_bound[0]), f32(delay_bound[1])
+        i += 1
+    p = np.clip(p, lo, hi)
+    N = p.shape[0]
+    tau = p[:, 0].astype(np.float64) if learn_tau else np.full(N, spec.tau)
+    delay = p[:, 1 if learn_tau else 0].astype(np.float64) if learn_delay else np.full(N, spec.delay)
+    return tau, delay, p[:, i:]
+
+
+def trajectory_learned(spec, params, s0, q0, qd0, learn_tau=False, learn_delay=False, sub_traj=False,
+                       tau_bound=None, delay_bound=None):
+    """Per-env phase (learned tau / delay): per-env tables built exactly as build_tables with the
+    env's (tau, delay), then `trajectory`.  With learn_sub_trajectories the plan has
+    T_e = round(tau_e / dt) samples (duration=None, black_box_wrapper.py:107-113; the length is
+    pinned by test_replanning_sequencing.py:99-107).  Returns pos, vel [N, T, dof] (NaN beyond
+    T_e) and T_e [N]."""
+    tau_bound = tau_bound or (2 * spec.dt, spec.duration)
+    delay_bound = delay_bound or (0.0, spec.duration - 2 * spec.dt)
+    tau, delay, w = learned_params(spec, params, learn_tau, learn_delay, tau_bound, delay_bound)
+    N, D = w.shape[0], spec.dof
+    s0 = np.broadcast_to(np.asarray(s0, np.int64), (N,))
+    q0 = np.asarray(q0, np.float64).reshape(N, D)
+    qd0 = np.asarray(qd0, np.float64).reshape(N, D)
+    Tmax = spec.T
+    pos = np.full((N, Tmax, D), np.nan, f32)
+    vel = np.full((N, Tmax, D), np.nan, f32)
+    lens = np.zeros(N, np.int64)
+    for i in range(N):
+        sp = replace(spec, tau=float(tau[i]), delay=float(delay[i]))
+        if sub_traj:
+            sp = replace(sp, T_override=int(np.round(tau[i] / spec.dt)))
+        Ti = sp.T
+        tabs = build_tables(sp, int(s0[i]) + Ti + 2)
+        p_, v_ = trajectory(sp, tabs, w[i:i + 1], s0[i:i + 1], q0[i:i + 1], qd0[i:i + 1])
+        pos[i, :Ti], vel[i, :Ti] = p_[0], v_[0]
+        lens[i] = Ti
+    return pos, vel, lens

@@ -90,3 +90,61 @@ def test_f64_division_by_reciprocal_is_exact():
     for x in xs:
         q = x * r
         assert fma(fma(-q, d, x), r, q) == x / d, x
+
+
+# ---------------------------------------------------------------- learned tau / delay (oracle side)
+def _learned(kind, phase, extra, lk, seed=0):
+    spec = mp.MPSpec(kind, 1, 5, phase, 1.5 if kind == "prodmp" else 2.0,
+                     zero_start=1 if kind == "promp" else 0, alpha=10.0)
+    p = np.random.default_rng(seed).standard_normal((1, spec.n_params + len(extra))).astype(np.float32)
+    p[0, :len(extra)] = extra
+    pos, vel, L = mp.trajectory_learned(spec, p, 0, np.zeros((1, 1)), np.zeros((1, 1)), **lk)
+    return pos[0, :L[0], 0], vel[0, :L[0], 0], int(L[0])
+
+
+@pytest.mark.parametrize("kind", ["promp", "prodmp"])
+@pytest.mark.parametrize("tau", [0.25, 0.5, 0.75, 1.0])
+def test_learn_tau_structure(kind, tau):
+    """test_black_box.py:219-255 on the restated MP: length 200, flat after tau (linear phase),
+    active section differs from the end."""
+    pos, vel, L = _learned(kind, "linear" if kind == "promp" else "exp", [tau], dict(learn_tau=True))
+    k = int(np.round(tau / 0.01))
+    assert L == 200
+    if kind == "promp":
+        assert np.all(pos[k:] == pos[-1]) and np.all(vel[k:] == vel[-1])
+    assert np.all(pos[:k - 1] != pos[-1]) and np.all(vel[:k - 2] != vel[-1])
+
+
+@pytest.mark.parametrize("delay", [0, 0.25, 0.5, 0.75])
+def test_learn_delay_structure(delay):
+    """test_black_box.py:258-297 (ProMP): constant during the delay, moving after it."""
+    pos, vel, L = _learned("promp", "linear", [delay], dict(learn_delay=True))
+    k = int(np.round(delay / 0.01))
+    assert L == 200
+    assert np.all(pos[:max(1, k - 1)] == pos[0]) and np.all(vel[:max(1, k - 2)] == vel[0])
+    assert np.all(pos[max(1, k):] != pos[0]) and np.all(vel[max(1, k)] != vel[0])
+
+
+@pytest.mark.parametrize("tau", [0.25, 0.5, 0.75, 1.0])
+@pytest.mark.parametrize("delay", [0.25, 0.5, 0.75, 1.0])
+def test_learn_tau_and_delay_structure(tau, delay):
+    """test_black_box.py:300-368 (ProMP)."""
+    if 2.0 < delay + tau:
+        return
+    pos, vel, L = _learned("promp", "linear", [tau, delay], dict(learn_tau=True, learn_delay=True))
+    kt, kd = int(np.round(tau / 0.01)), int(np.round(delay / 0.01))
+    kj = kt + kd
+    assert np.all(pos[kj:] == pos[-1]) and np.all(vel[kj:] == vel[-1])
+    assert np.all(pos[:kd - 1] == pos[0]) and np.all(vel[:kd - 2] == vel[0])
+    ap, av = pos[kd:kj - 1], vel[kd:kj - 2]
+    assert np.all(ap != pos[-1]) and np.all(ap != pos[0])
+    assert np.all(av != vel[-1]) and np.all(av != vel[0])
+
+
+@pytest.mark.parametrize("kind", ["promp", "dmp"])
+def test_sub_trajectory_length(kind):
+    """test_replanning_sequencing.py:99-107: length == round(tau / dt), tau clipped to [2dt, D]."""
+    for tau in (0.013, 0.02, 0.37, 1.234, 2.0, 7.0):
+        _, _, L = _learned(kind, "exp", [tau], dict(sub_traj=True, learn_tau=True))
+        t = float(np.clip(np.float32(tau), np.float32(0.02), np.float32(2.0)))
+        assert L == int(np.round(t / 0.01))

@@ -114,3 +114,51 @@ def test_batched_vs_port_features():
                 np.testing.assert_array_equal(inf["positions"], info["positions"][i])
                 if t1 or t2:
                     np.testing.assert_array_equal(p.reset(), obs[i])
+
+
+LEARNED = [
+    ("LongSimpleReacher", ("pd", 0.6, 0.075), mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1),
+     dict(learn_tau=True)),
+    ("SimpleReacher", ("pd", 0.6, 0.075), mp.MPSpec("dmp", 2, 5, "exp", 2.0, alpha_phase=2.0, weights_scale=50),
+     dict(learn_tau=True, learn_delay=True)),
+    ("HoleReacher", ("pd", 1.0, 0.1), mp.MPSpec("prodmp", 5, 5, "exp", 1.5, alpha=10.0), dict(learn_tau=True)),
+    ("SimpleReacher", ("pd", 0.6, 0.075), mp.MPSpec("promp", 2, 5, "linear", 2.0, zero_start=1),
+     dict(sub_traj=True)),
+    ("ViaPointReacher", ("vel",), mp.MPSpec("promp", 5, 5, "linear", 2.0, zero_start=1), dict(learn_delay=True)),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(LEARNED)))
+def test_batched_vs_port_learned_phase(ci):
+    """learn_tau / learn_delay / learn_sub_trajectories (make_env_helpers.py:115-126,
+    black_box_wrapper.py:106-119): per-env phase parameters at the front of the params."""
+    name, ctrl, spec, lk = LEARNED[ci]
+    E = 6
+    sub = lk.get("sub_traj", False)
+    n_extra = int(lk.get("learn_tau", False) or sub) + int(lk.get("learn_delay", False))
+    bb = batched.BatchedBB(name, E, ctrl, mp_spec=spec, info_level=2, learned=lk)
+    def fn(params, t0, cp, cv):   # one env's plan, cut to its length T_e
+        pos, vel, lens = mp.trajectory_learned(
+            spec, params[None], int(round(t0 / 0.01)), cp[None], cv[None],
+            learn_tau=lk.get("learn_tau", False) or sub, learn_delay=lk.get("learn_delay", False), sub_traj=sub)
+        return pos[0, :lens[0]], vel[0, :lens[0]]
+
+    ports = []
+    for i in range(E):
+        c = port.PD(ctrl[1], ctrl[2]) if ctrl[0] == "pd" else port.Vel()
+        ports.append(port.BlackBoxPort(port.Reacher(name), fn, c, learn_sub_trajectories=sub))
+    np.testing.assert_array_equal(bb.reset(seed=21), np.array([p.reset(seed=21 + i) for i, p in enumerate(ports)]))
+    rng = np.random.default_rng(2)
+    for b in range(4):
+        params = rng.standard_normal((E, spec.n_params + n_extra), dtype=np.float32)
+        params[:, :n_extra] = rng.uniform(0.0, 2.2, (E, n_extra)).astype(np.float32)   # some clipped
+        obs, ret, te, tr, info = bb.step(params)
+        for i, p in enumerate(ports):
+            o, r, t1, t2, inf = p.step(params[i])
+            assert r == ret[i] and t1 == te[i] and t2 == tr[i]
+            assert inf["trajectory_length"] == info["trajectory_length"][i]
+            np.testing.assert_array_equal(o, info["final_obs"][i])
+            L = len(inf["positions"])
+            np.testing.assert_array_equal(inf["positions"], info["positions"][i, :L])
+            if t1 or t2:
+                np.testing.assert_array_equal(p.reset(), obs[i])
