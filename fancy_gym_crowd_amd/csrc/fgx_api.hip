@@ -15,6 +15,7 @@
 #include "fgx_tables.h"
 #include "fgx_aux.h"
 #include "fgx_dispatch.h"
+#include "fgx_learned.h"
 
 using namespace fgx;
 
@@ -42,6 +43,13 @@ struct Handle {
   double* scratch = nullptr;
   void* state_block = nullptr;
   int ctx_dim = 0;
+  // learned tau / delay: per-env tables, plans and plan lengths
+  float* env_tab = nullptr;
+  float* plan_pos = nullptr;
+  float* plan_vel = nullptr;
+  int32_t* plan_len = nullptr;
+  void* learned_block = nullptr;
+  bool learned() const { return dc.learn_tau || dc.learn_delay; }
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -74,6 +82,26 @@ static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* m
   return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
 }
 
+static int launch_traj_env(const Handle& h, const float* params, float* pos, float* vel, hipStream_t stream) {
+  const int threads = 256;
+  const int blocks = (int)((h.dc.N + threads - 1) / threads);
+#define LAUNCH(MPV, NLV)                                                                                       \
+  hipLaunchKernelGGL((k_traj_env<MPV, NLV, 5>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, params,    \
+                     h.env_tab, pos, vel, h.plan_len)
+  const int mp = h.dc.mp, nl = h.dc.nl;
+  if (h.dc.nb != 5) return fail(FGX_E_UNSUPPORTED, "n_basis != 5 not instantiated");
+  if (mp == MP_PROMP && nl == 2) LAUNCH(MP_PROMP, 2);
+  else if (mp == MP_PROMP && nl == 5) LAUNCH(MP_PROMP, 5);
+  else if (mp == MP_DMP && nl == 2) LAUNCH(MP_DMP, 2);
+  else if (mp == MP_DMP && nl == 5) LAUNCH(MP_DMP, 5);
+  else if (mp == MP_PRODMP && nl == 2) LAUNCH(MP_PRODMP, 2);
+  else if (mp == MP_PRODMP && nl == 5) LAUNCH(MP_PRODMP, 5);
+  else return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+#undef LAUNCH
+  HIP_TRY(hipGetLastError());
+  return FGX_OK;
+}
+
 // ------------------------------------------------------------------------ config -> DevCfg
 static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim) {
   if (c.abi_version != FGX_ABI_VERSION) return fail(FGX_E_INVALID, "abi_version mismatch");
@@ -84,8 +112,16 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   if (c.rew_fct != FGX_REW_SIMPLE && c.env_kind != FGX_ENV_HOLE) return fail(FGX_E_INVALID, "rew_fct is a HoleReacher option");
   if (c.learn_sub_trajectories && c.replan_period > 0)   // make_env_helpers.py:91-92
     return fail(FGX_E_INVALID, "Cannot used sub-trajectory learning and replanning together.");
-  if (c.learn_tau || c.learn_delay || c.learn_sub_trajectories)
-    return fail(FGX_E_UNSUPPORTED, "learn_tau / learn_delay / learn_sub_trajectories not implemented yet");
+  if (c.learn_sub_trajectories && !c.learn_tau)   // make_env_helpers.py:115-116
+    return fail(FGX_E_INVALID, "learn_sub_trajectories requires learn_tau");
+  if ((c.learn_tau || c.learn_delay) && c.mp_kind == FGX_MP_NONE)
+    return fail(FGX_E_INVALID, "learn_tau / learn_delay need a movement primitive");
+  if (c.learn_delay && c.mp_kind == FGX_MP_PRODMP)
+    return fail(FGX_E_UNSUPPORTED, "prodmp with a learned delay");
+  if (c.learn_tau && !(c.tau_bound_lo > 0.0 && c.tau_bound_lo <= c.tau_bound_hi))
+    return fail(FGX_E_INVALID, "tau_bound must satisfy 0 < lo <= hi");
+  if (c.learn_delay && !(c.delay_bound_lo >= 0.0 && c.delay_bound_lo <= c.delay_bound_hi))
+    return fail(FGX_E_INVALID, "delay_bound must satisfy 0 <= lo <= hi");
   if (c.n_links < 1 || c.n_links > kMaxLinks) return fail(FGX_E_INVALID, "n_links out of range");
   if (c.mp_kind < FGX_MP_NONE || c.mp_kind > FGX_MP_PRODMP) return fail(FGX_E_INVALID, "bad mp_kind");
   if (c.ctrl_kind < FGX_CTRL_PD || c.ctrl_kind > FGX_CTRL_POS) return fail(FGX_E_INVALID, "bad ctrl_kind");
@@ -144,6 +180,12 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.out_dim = c.return_context ? ctx_dim : d.full_dim;
   d.n_params = (c.mp_kind == FGX_MP_PROMP) ? n * c.n_basis : n * (c.n_basis + 1);
   if (c.mp_kind == FGX_MP_NONE) d.n_params = 0;
+  d.n_params += (c.learn_tau ? 1 : 0) + (c.learn_delay ? 1 : 0);   // params = [tau?, delay?, w...]
+  d.learn_tau = c.learn_tau != 0;
+  d.learn_delay = c.learn_delay != 0;
+  d.sub_traj = c.learn_sub_trajectories != 0;
+  d.tau_lo32 = (float)c.tau_bound_lo; d.tau_hi32 = (float)c.tau_bound_hi;
+  d.delay_lo32 = (float)c.delay_bound_lo; d.delay_hi32 = (float)c.delay_bound_hi;
   const int max_s0 = c.replan_period > 0 ? c.max_episode_steps : 0;
   d.rows = max_s0 + c.T + 2;
   if (c.mp_kind == FGX_MP_PRODMP) {
@@ -167,6 +209,9 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.tgt_x0 = c.target_x; d.tgt_y0 = c.target_y;
   d.dt = c.dt;
   d.tau = c.tau;
+  d.delay = c.delay;
+  d.alpha_phase = c.alpha_phase;
+  d.bandwidth = c.bandwidth;
   d.p_gain = c.p_gain;
   d.d_gain = c.d_gain;
   d.act_lo = c.act_low;
@@ -246,6 +291,21 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.plan_len = nullptr;
   h->st.tables = h->tables;
   (void)hipMemset(h->state_block, 0, off);
+  if (h->learned()) {
+    const DevCfg& d0 = h->dc;
+    size_t lo = 0;
+    const size_t o_et = lo; lo = align_up(lo + sizeof(float) * (size_t)N * d0.rows * d0.stride);
+    const size_t o_pp = lo; lo = align_up(lo + sizeof(float) * (size_t)N * d0.T * nl);
+    const size_t o_pv = lo; lo = align_up(lo + sizeof(float) * (size_t)N * d0.T * nl);
+    const size_t o_pl = lo; lo = align_up(lo + sizeof(int32_t) * N);
+    e = hipMalloc(&h->learned_block, lo);
+    if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_NOMEM, "hipMalloc per-env plans"); }
+    char* lb = (char*)h->learned_block;
+    h->env_tab = (float*)(lb + o_et);
+    h->plan_pos = (float*)(lb + o_pp);
+    h->plan_vel = (float*)(lb + o_pv);
+    h->plan_len = (int32_t*)(lb + o_pl);
+  }
   // basis tables
   const DevCfg& d = h->dc;
   if (d.mp == MP_PROMP || d.mp == MP_DMP) {
@@ -282,6 +342,7 @@ int fgx_destroy(void* handle) {
   if (!h) return FGX_OK;
   (void)hipSetDevice(h->device);
   if (h->state_block) (void)hipFree(h->state_block);
+  if (h->learned_block) (void)hipFree(h->learned_block);
   if (h->scratch) (void)hipFree(h->scratch);
   delete h;
   return FGX_OK;
@@ -344,6 +405,19 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
   if (info && ((info->reward_dist == nullptr) != (info->reward_ctrl == nullptr)))
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
+  if (h->learned()) {
+    // per-env plans first (written straight into the info buffers when those are requested),
+    // then the episode over the given plans with per-env lengths
+    float* P = (info && info->positions) ? info->positions : h->plan_pos;
+    float* V = (info && info->velocities) ? info->velocities : h->plan_vel;
+    int rc = launch_traj_env(*h, params, P, V, (hipStream_t)stream);
+    if (rc) return rc;
+    Handle hh = *h;
+    hh.st.plan_len = h->plan_len;
+    o.positions = nullptr;
+    o.velocities = nullptr;
+    return launch_episode(hh, MP_GIVEN, nullptr, P, V, o, (hipStream_t)stream);
+  }
   return launch_episode(*h, h->dc.mp, params, nullptr, nullptr, o, (hipStream_t)stream);
 }
 
@@ -369,6 +443,7 @@ int fgx_trajectory(void* handle, const float* params, float* des_pos, float* des
   Handle* h = (Handle*)handle;
   if (!h) return fail(FGX_E_INVALID, "null handle");
   if (!params || !des_pos || !des_vel) return fail(FGX_E_INVALID, "null argument");
+  if (h->learned()) return launch_traj_env(*h, params, des_pos, des_vel, (hipStream_t)stream);
   return launch_trajectory(h->dc, h->st, params, des_pos, des_vel, (hipStream_t)stream, g_err);
 }
 

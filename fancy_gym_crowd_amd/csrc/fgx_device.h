@@ -39,12 +39,15 @@ struct DevCfg {
   int n_params, rows, stride;
   int rand_width, rand_x, rand_depth;
   int rew_fct;      // HoleReacher reward function (REW_*)
+  int learn_tau, learn_delay, sub_traj;   // per-env phase parameters at the front of params
   int rand_via, rand_target;   // ViaPointReacher: via point / target sampled at reset
   int ctx_idx[kMaxObs + 1];
   double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;
   float act_lo32, act_hi32, dt32, rcp_dt32, tau32, rcp_tau32;
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
   double via_x0, via_y0, tgt_x0, tgt_y0;
+  double delay, alpha_phase, bandwidth;   // phase / basis generator (per-env tables)
+  float tau_lo32, tau_hi32, delay_lo32, delay_hi32;   // action-space bounds of tau / delay
   float ws32, gs32, alpha32, beta32;
   double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
 };

@@ -99,7 +99,9 @@ __global__ __launch_bounds__(256) void k_reset(DevCfg c, DevState s, const uint6
 
 // ============================================================================ trajectories
 // Per-thread desired-trajectory generator (oracle/mp.py:trajectory), f32 throughout.
-template <int MP, int NL, int NB>
+// DIVREF: divide by tau with the IEEE division (per-env learned tau, for which the reciprocal
+// shortcut div_rcp is not verified) instead of div_rcp.
+template <int MP, int NL, int NB, bool DIVREF = false>
 struct Traj {
   static constexpr int K = (MP == MP_PRODMP) ? NB + 3 : NB;
   float w[NL][K];          // ProMP: w ; DMP: w' ; ProDMP: [w', g', c1, c2]
@@ -108,6 +110,9 @@ struct Traj {
   float cur[NL], vprev[NL];// ProMP look-ahead
   const float* tab;
   int stride, s0, T;
+  float tau32, rtau32;
+
+  __device__ __forceinline__ float div_tau(float x) const { return DIVREF ? x / tau32 : div_rcp(x, tau32, rtau32); }
 
   __device__ __forceinline__ static float chain(const float* row, const float* wd) {
     float acc = 0.0f;
@@ -119,7 +124,12 @@ struct Traj {
   // params: this env's row of the [N, n_params] matrix; q0/qd0 the initial conditions
   __device__ __forceinline__ void init(const DevCfg& c, const float* params, const float* tab_, int s0_,
                                        const double* q0, const double* qd0) {
-    tab = tab_; stride = c.stride; s0 = s0_; T = c.T;
+    init(c, params, tab_, s0_, q0, qd0, c.T, c.tau32, c.rcp_tau32);
+  }
+  // T_ / tau32_: this plan's length and tau (learned tau, sub-trajectories)
+  __device__ __forceinline__ void init(const DevCfg& c, const float* params, const float* tab_, int s0_,
+                                       const double* q0, const double* qd0, int T_, float tau32_, float rtau32_) {
+    tab = tab_; stride = c.stride; s0 = s0_; T = T_; tau32 = tau32_; rtau32 = rtau32_;
     if (MP == MP_PROMP) {
 #pragma unroll
       for (int d = 0; d < NL; ++d)
@@ -135,7 +145,7 @@ struct Traj {
         for (int j = 0; j < NB; ++j) w[d][j] = params[d * NB + j] * c.ws32;
         g[d] = params[NL * NB + d] * c.gs32;
         y[d] = (float)q0[d];
-        z[d] = (float)qd0[d] * c.tau32;
+        z[d] = (float)qd0[d] * tau32;
       }
     } else if (MP == MP_PRODMP) {
       const float* rb = tab + (size_t)s0 * stride;
@@ -153,7 +163,7 @@ struct Traj {
           V = __builtin_fmaf(rb[NB + 1 + j], w[d][j], V);
         }
         const float A = (float)q0[d] - P;
-        const float B = (float)qd0[d] * c.tau32 - V;
+        const float B = (float)qd0[d] * tau32 - V;
         w[d][NB + 1] = (dy2 * A - y2 * B) / det;
         w[d][NB + 2] = (y1 * B - dy1 * A) / det;
       }
@@ -185,7 +195,7 @@ struct Traj {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         pos[d] = y[d];
-        vel[d] = div_rcp(z[d], c.tau32, c.rcp_tau32);
+        vel[d] = div_tau(z[d]);
         if (k < T - 1) {
           const float f = chain(row, w[d]);
           const float acc = c.alpha32 * (c.beta32 * (g[d] - y[d]) - z[d]) + f;
@@ -202,7 +212,7 @@ struct Traj {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         pos[d] = chain(hp, w[d]);
-        vel[d] = div_rcp(chain(hv, w[d]), c.tau32, c.rcp_tau32);
+        vel[d] = div_tau(chain(hv, w[d]));
       }
     }
   }

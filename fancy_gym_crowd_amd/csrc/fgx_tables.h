@@ -45,15 +45,13 @@ __device__ inline void rbf64(const DevCfg& c, double alpha_x, double bw, double 
   for (int j = 0; j < n; ++j) phi[j] = e[j] / s;
 }
 
-// ProMP / DMP tables: one thread per row.
-__global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x, double bw, float* tab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.rows) return;
+// One ProMP / DMP table row i (t_i = i*dt) for the phase (tau, delay).
+__device__ inline void rbf_row(const DevCfg& c, int i, double tau, double delay, double alpha_x, double bw,
+                               float* row) {
   double phi[kMaxBasis + 4];
   const double t = (double)i * c.dt;
   const double x = phase64(c, t, tau, delay, alpha_x);
   rbf64(c, alpha_x, bw, x, phi);
-  float* row = tab + (size_t)i * c.stride;
   if (c.mp == MP_PROMP) {
     for (int j = 0; j < c.nb; ++j) row[j] = (float)(c.weights_scale * phi[c.zs + j]);
     const float t0 = (float)t, t1 = (float)((double)(i + 1) * c.dt);
@@ -69,22 +67,79 @@ __global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x,
   }
 }
 
+// ProMP / DMP tables: one thread per row.
+__global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x, double bw, float* tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.rows) return;
+  rbf_row(c, i, tau, delay, alpha_x, bw, tab + (size_t)i * c.stride);
+}
+
+// ProDMP fine-grid pieces at s = i*h (oracle/mp.py:prodmp_fine64): the variation-of-parameters
+// integrands k1*phi, k2*phi and the homogeneous solutions.
+__device__ inline void prodmp_integrands(const DevCfg& c, double s, double alpha_x, double bw, double* d1,
+                                         double* d2) {
+  const double x = exp((-alpha_x) * s);
+  double phi[kMaxBasis + 4];
+  rbf64(c, alpha_x, bw, x, phi);
+  const double e = exp(c.alpha * s / 2);
+  const double k1 = s * e * x, k2 = e * x;
+  for (int j = 0; j < c.nb; ++j) {
+    d1[j] = k1 * phi[c.zs + j];
+    d2[j] = k2 * phi[c.zs + j];
+  }
+}
+
+// ProDMP table row from the cumulative integrals p1, p2 at s.
+__device__ inline void prodmp_row(const DevCfg& c, double s, const double* p1, const double* p2, float* row) {
+  const int nb = c.nb;
+  const double a = c.alpha;
+  const double e = exp(a * s / 2);
+  const double y1 = exp((-a) * s / 2);
+  const double y2 = s * y1;
+  const double dy1 = -a / 2 * y1;
+  const double dy2 = -a / 2 * y2 + y1;
+  const double q1 = (a * s / 2 - 1) * e + 1;
+  const double q2 = a / 2 * (e - 1);
+  for (int j = 0; j < nb; ++j) {
+    row[j] = (float)(p2[j] * y2 - p1[j] * y1);
+    row[nb + 1 + j] = (float)(p2[j] * dy2 - p1[j] * dy1);
+  }
+  row[nb] = (float)(q2 * y2 - q1 * y1);
+  row[2 * nb + 1] = (float)(q2 * dy2 - q1 * dy1);
+  row[2 * nb + 2] = (float)y1;
+  row[2 * nb + 3] = (float)y2;
+  row[2 * nb + 4] = (float)dy1;
+  row[2 * nb + 5] = (float)dy2;
+}
+
+// One env's ProDMP rows 0..R-1 for its own tau, sequentially in one thread (the cumulative
+// trapezoid in the same order as k_tables_prodmp / the oracle).
+__device__ inline void prodmp_rows_seq(const DevCfg& c, double tau, double alpha_x, double bw, int R, float* tab) {
+  const int nb = c.nb;
+  const double h = c.dt / tau;
+  double p1[kMaxBasis], p2[kMaxBasis], prev1[kMaxBasis], prev2[kMaxBasis], cur1[kMaxBasis], cur2[kMaxBasis];
+  prodmp_integrands(c, 0.0, alpha_x, bw, prev1, prev2);
+  for (int j = 0; j < nb; ++j) { p1[j] = 0.0; p2[j] = 0.0; }
+  prodmp_row(c, 0.0, p1, p2, tab);
+  for (int i = 1; i < R; ++i) {
+    const double s = (double)i * h;
+    prodmp_integrands(c, s, alpha_x, bw, cur1, cur2);
+    for (int j = 0; j < nb; ++j) {
+      p1[j] = p1[j] + h * (prev1[j] + cur1[j]) / 2;
+      p2[j] = p2[j] + h * (prev2[j] + cur2[j]) / 2;
+      prev1[j] = cur1[j];
+      prev2[j] = cur2[j];
+    }
+    prodmp_row(c, s, p1, p2, tab + (size_t)i * c.stride);
+  }
+}
+
 // ProDMP precompute (oracle/mp.py:prodmp_fine64).  Single block; scratch: [rows][2*nb] f64.
 __global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw, double* dp, float* tab) {
   const int nb = c.nb, R = c.rows, W = 2 * nb;
-  const double h = c.dt / tau, a = c.alpha;
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {
-    const double s = (double)i * h;
-    const double x = exp((-alpha_x) * s);
-    double phi[kMaxBasis + 4];
-    rbf64(c, alpha_x, bw, x, phi);
-    const double e = exp(a * s / 2);
-    const double k1 = s * e * x, k2 = e * x;
-    for (int j = 0; j < nb; ++j) {
-      dp[(size_t)i * W + j] = k1 * phi[c.zs + j];
-      dp[(size_t)i * W + nb + j] = k2 * phi[c.zs + j];
-    }
-  }
+  const double h = c.dt / tau;
+  for (int i = threadIdx.x; i < R; i += blockDim.x)
+    prodmp_integrands(c, (double)i * h, alpha_x, bw, dp + (size_t)i * W, dp + (size_t)i * W + nb);
   __syncthreads();
   // cumulative trapezoid, one thread per column, sequential (same order as the oracle)
   if ((int)threadIdx.x < W) {
@@ -99,28 +154,8 @@ __global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw,
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {
-    const double s = (double)i * h;
-    const double e = exp(a * s / 2);
-    const double y1 = exp((-a) * s / 2);
-    const double y2 = s * y1;
-    const double dy1 = -a / 2 * y1;
-    const double dy2 = -a / 2 * y2 + y1;
-    const double q1 = (a * s / 2 - 1) * e + 1;
-    const double q2 = a / 2 * (e - 1);
-    float* row = tab + (size_t)i * c.stride;
-    for (int j = 0; j < nb; ++j) {
-      const double p1 = dp[(size_t)i * W + j], p2 = dp[(size_t)i * W + nb + j];
-      row[j] = (float)(p2 * y2 - p1 * y1);
-      row[nb + 1 + j] = (float)(p2 * dy2 - p1 * dy1);
-    }
-    row[nb] = (float)(q2 * y2 - q1 * y1);
-    row[2 * nb + 1] = (float)(q2 * dy2 - q1 * dy1);
-    row[2 * nb + 2] = (float)y1;
-    row[2 * nb + 3] = (float)y2;
-    row[2 * nb + 4] = (float)dy1;
-    row[2 * nb + 5] = (float)dy2;
-  }
+  for (int i = threadIdx.x; i < R; i += blockDim.x)
+    prodmp_row(c, (double)i * h, dp + (size_t)i * W, dp + (size_t)i * W + nb, tab + (size_t)i * c.stride);
 }
 
 }  // namespace fgx

@@ -274,10 +274,11 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     # ---- make_bb (make_env_helpers.py:68-136)
     if bb.get('learn_sub_trajectories') and bb.get('replanning_schedule'):
         raise ValueError('Cannot used sub-trajectory learning and replanning together.')
-    if bb.get('learn_sub_trajectories'):
-        raise NotImplementedError("learn_sub_trajectories (per-env tau) is not implemented on the device yet")
-    if ph.get('learn_tau') or ph.get('learn_delay'):
-        raise NotImplementedError("learn_tau / learn_delay (per-env phase) are not implemented on the device yet")
+    learn_sub = bool(bb.get('learn_sub_trajectories'))
+    learn_tau = bool(ph.get('learn_tau', False))
+    learn_delay = bool(ph.get('learn_delay', False))
+    if bb.get('learn_sub_trajectories') is not None:   # make_env_helpers.py:115-116 ("is not None")
+        learn_tau = True
     duration = bb.get('duration')
     if duration is None:
         duration = c.max_episode_steps * c.dt
@@ -290,7 +291,8 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     if action_dim != n:
         raise ValueError("action_dim must equal n_links for the reacher envs")
     period = _schedule_period(bb.get('replanning_schedule'), c.max_episode_steps)
-    time_aware = period > 0 or any(getattr(w, '__name__', '') == 'TimeAwareObservation' for w in wrappers)
+    time_aware = (period > 0 or learn_sub or
+                  any(getattr(w, '__name__', '') == 'TimeAwareObservation' for w in wrappers))
 
     tg_type = tg.get('trajectory_generator_type', '').lower()
     ph_type = ph.get('phase_generator_type', '').lower()
@@ -342,7 +344,15 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c.max_planning_times = 0 if mpt is None or mpt == math.inf else int(mpt)
     c.condition_on_desired = int(bool(bb.get('condition_on_desired', False)))
     c.time_aware = int(time_aware)
-    c.return_context = int(not (period > 0 or bb.get('learn_sub_trajectories')))
+    c.return_context = int(not (period > 0 or learn_sub))
+    # learned phase parameters (make_env_helpers.py:115-126): bounds two env steps .. duration
+    c.learn_tau, c.learn_delay, c.learn_sub_trajectories = int(learn_tau), int(learn_delay), int(learn_sub)
+    tb = ph.get('tau_bound') or [c.dt * 2, duration]
+    db = ph.get('delay_bound') or [0, duration - c.dt * 2]
+    c.tau_bound_lo, c.tau_bound_hi = float(tb[0]), float(tb[1])
+    c.delay_bound_lo, c.delay_bound_hi = float(db[0]), float(db[1])
+    if learn_delay and tg_type == 'prodmp':
+        raise NotImplementedError("ProDMP with learn_delay")
     agg = bb.get('reward_aggregation', np.sum)
     if agg is np.sum:
         meta['reward_aggregation'] = 'sum'
@@ -351,5 +361,5 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     else:
         raise NotImplementedError("reward_aggregation other than np.sum / np.mean")
     meta['verbose'] = int(bb.get('verbose', 1))
-    meta['n_params'] = n * c.n_basis + (0 if tg_type == 'promp' else n)
+    meta['n_params'] = n * c.n_basis + (0 if tg_type == 'promp' else n) + int(learn_tau) + int(learn_delay)
     return c, meta

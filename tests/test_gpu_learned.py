@@ -1,0 +1,124 @@
+"""GPU parity for learned phase parameters (make_env_helpers.py:115-126): learn_tau,
+learn_delay and learn_sub_trajectories (black_box_wrapper.py:106-119), against
+oracle.mp.trajectory_learned through the vectorised oracle.
+
+Per-env basis tables are computed on the device in f64 and rounded once to f32, like the
+shared tables (<= 1 ulp from numpy's exp, test_gpu_parity.py::test_tables_within_one_ulp), so
+plans, observations and returns are compared within the north_star tolerance (1e-5
+relative); plan lengths, flags and step counts exactly.  The MP numerics themselves are parity
+unpinned (mp_pytorch is not in the container); the structural properties the reference's
+tests assert (test_black_box.py:219-368, test_replanning_sequencing.py:64-107) are checked on
+the device output.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fancy_gym_crowd_amd as fgx
+from oracle import batched
+from tests.test_gpu_parity import close, ctrl_of, np_, oracle_kwargs, spec_of
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+CASES = [
+    ("fancy_ProMP/LongSimpleReacher-v0", {"phase_generator_kwargs": {"learn_tau": True}}, {}, 256, 3),
+    ("fancy_DMP/SimpleReacher-v0", {"phase_generator_kwargs": {"learn_tau": True, "learn_delay": True}}, {}, 256, 3),
+    ("fancy_ProDMP/HoleReacher-v0", {"phase_generator_kwargs": {"learn_tau": True}}, {}, 128, 3),
+    ("fancy_ProMP/SimpleReacher-v0", {"black_box_kwargs": {"learn_sub_trajectories": True}}, {}, 256, 6),
+    ("fancy_DMP/HoleReacher-v0", {"black_box_kwargs": {"learn_sub_trajectories": True}}, {}, 128, 6),
+    ("fancy_ProMP/ViaPointReacher-v0", {"phase_generator_kwargs": {"learn_delay": True}}, {}, 128, 2),
+    ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"learn_sub_trajectories": True}}, {}, 128, 6),
+]
+NAME = {"SimpleReacher-v0": "SimpleReacher", "LongSimpleReacher-v0": "LongSimpleReacher",
+        "HoleReacher-v0": "HoleReacher", "ViaPointReacher-v0": "ViaPointReacher"}
+
+
+def _learned_kw(env):
+    c = env._eng.cfg
+    return dict(learn_tau=bool(c.learn_tau), learn_delay=bool(c.learn_delay), sub_traj=bool(c.learn_sub_trajectories),
+                tau_bound=(c.tau_bound_lo, c.tau_bound_hi), delay_bound=(c.delay_bound_lo, c.delay_bound_hi))
+
+
+@pytest.mark.parametrize("ci", range(len(CASES)))
+@pytest.mark.parametrize("info_level", [0, 2])
+def test_learned_phase_vs_oracle(ci, info_level):
+    env_id, over, kw, N, n_bb = CASES[ci]
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    spec = spec_of(env)
+    lk = _learned_kw(env)
+    n_extra = int(lk["learn_tau"]) + int(lk["learn_delay"])
+    assert env.n_params == spec.n_params + n_extra
+    ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=info_level,
+                           learned=lk, env_kwargs=kw, **oracle_kwargs(env))
+    close(np_(env.reset(seed=40)[0]), ob.reset(seed=40))
+    rng = np.random.default_rng(12)
+    for b in range(n_bb):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        params[:, :n_extra] = rng.uniform(-0.1, 2.2, (N, n_extra)).astype(np.float32)   # some clipped
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        np.testing.assert_array_equal(np_(te), r_te)
+        np.testing.assert_array_equal(np_(tr), r_tr)
+        close(np_(ret), r_ret)
+        close(np_(info["final_observation"]), r_info["final_obs"])
+        close(np_(obs), r_obs)
+        st = env.get_state()
+        np.testing.assert_array_equal(np_(st["steps"]), ob.env.steps)
+        close(np_(st["q"]), ob.env.q)
+        if info_level >= 2:
+            p, rp = np_(info["positions"]), r_info["positions"]
+            np.testing.assert_array_equal(np.isnan(p), np.isnan(rp))     # plan lengths (NaN beyond)
+            close(p[~np.isnan(p)], rp[~np.isnan(rp)])
+            close(np_(info["velocities"])[~np.isnan(p)], r_info["velocities"][~np.isnan(rp)])
+
+
+def _plan(env_id, over, extra):
+    env = fgx.make(env_id, num_envs=4, device=DEV, mp_config_override=over, info_level=2)
+    env.reset(seed=0)
+    params = np.random.default_rng(0).standard_normal((4, env.n_params)).astype(np.float32)
+    params[:, :len(extra)] = extra
+    obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+    return np_(info["positions"])[:, :, 0], np_(info["velocities"])[:, :, 0], np_(info["trajectory_length"])
+
+
+@pytest.mark.parametrize("mp", ["ProMP", "ProDMP"])
+@pytest.mark.parametrize("tau", [0.25, 0.5, 0.75, 1.0])
+def test_learn_tau_structure_on_device(mp, tau):
+    """test_black_box.py:219-255 on the device plans (first joint of LongSimpleReacher)."""
+    pos, vel, L = _plan(f"fancy_{mp}/LongSimpleReacher-v0", {"phase_generator_kwargs": {"learn_tau": True}}, [tau])
+    k = int(np.round(tau / 0.01))
+    assert np.all(L == 200)
+    for i in range(4):
+        if mp == "ProMP":
+            assert np.all(pos[i, k:] == pos[i, -1]) and np.all(vel[i, k:] == vel[i, -1])
+        assert np.all(pos[i, :k - 1] != pos[i, -1]) and np.all(vel[i, :k - 2] != vel[i, -1])
+
+
+@pytest.mark.parametrize("delay", [0, 0.25, 0.5, 0.75])
+def test_learn_delay_structure_on_device(delay):
+    """test_black_box.py:258-297 (ProMP) on the device plans."""
+    pos, vel, L = _plan("fancy_ProMP/LongSimpleReacher-v0", {"phase_generator_kwargs": {"learn_delay": True}}, [delay])
+    k = int(np.round(delay / 0.01))
+    for i in range(4):
+        assert np.all(pos[i, :max(1, k - 1)] == pos[i, 0]) and np.all(vel[i, :max(1, k - 2)] == vel[i, 0])
+        assert np.all(pos[i, max(1, k):] != pos[i, 0]) and np.all(vel[i, max(1, k)] != vel[i, 0])
+
+
+@pytest.mark.parametrize("mp", ["ProMP", "DMP"])
+def test_sub_trajectory_lengths_on_device(mp):
+    """test_replanning_sequencing.py:99-107: length == round(tau / dt) unless the episode ends."""
+    env = fgx.make(f"fancy_{mp}/SimpleReacher-v0", num_envs=64, device=DEV,
+                   mp_config_override={"black_box_kwargs": {"learn_sub_trajectories": True}})
+    env.reset(seed=1)
+    rng = np.random.default_rng(3)
+    for _ in range(25):
+        params = rng.standard_normal((64, env.n_params)).astype(np.float32)
+        params[:, 0] = rng.uniform(0.0, 2.5, 64)
+        _, _, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        L = np_(info["trajectory_length"])
+        want = np.round(np.clip(params[:, 0], np.float32(0.02), np.float32(2.0)).astype(np.float64) / 0.01)
+        done = np_(te) | np_(tr)
+        assert np.all(L[~done] == want[~done])
+        assert np.all(L[done] <= want[done])
