@@ -13,10 +13,11 @@ utils/make_env_helpers.py:68-136) and returns a batched env whose every step run
 hand-written HIP kernels (libfgx.so) on the GPU.
 """
 from .registry import (ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS, ENV_SPECS, KNOWN_MPS,  # noqa: F401
-                       MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS, ReplanEvery, nested_update, register,
-                       resolve, upgrade)
+                       MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS, REPLAN_CLOSE, ReplanAny, ReplanAt,
+                       ReplanEvery, ReplanNormPeriod, nested_update, register, resolve, upgrade)
 
-__all__ = ["make", "BlackBoxVectorEnv", "StepVectorEnv", "ReplanEvery", "register", "upgrade", "resolve",
+__all__ = ["make", "BlackBoxVectorEnv", "StepVectorEnv", "ReplanEvery", "ReplanAt", "ReplanNormPeriod",
+           "ReplanAny", "REPLAN_CLOSE", "register", "upgrade", "resolve",
            "ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS", "KNOWN_MPS"]
 
 

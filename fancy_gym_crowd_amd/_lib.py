@@ -11,9 +11,10 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 2
+FGX_ABI_VERSION = 3
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
+SCHED_EVERY, SCHED_AT, SCHED_NORM_PERIOD = 0, 1, 2
 MP_NONE, MP_PROMP, MP_DMP, MP_PRODMP = 0, 1, 2, 3
 PHASE_LINEAR, PHASE_EXP = 0, 1
 CTRL_PD, CTRL_VEL, CTRL_POS = 0, 1, 2
@@ -34,7 +35,10 @@ class FgxConfig(ctypes.Structure):
             "rew_fct", "learn_tau", "learn_delay", "learn_sub_trajectories")] + [
         (n, ctypes.c_double) for n in (
             "tau_bound_lo", "tau_bound_hi", "delay_bound_lo", "delay_bound_hi",
-            "via_x", "via_y", "target_x", "target_y")]
+            "via_x", "via_y", "target_x", "target_y")] + [
+        ("sched_n", ctypes.c_int32), ("sched_kind", ctypes.c_int32 * 4), ("sched_k", ctypes.c_int32 * 4),
+        ("sched_i0", ctypes.c_int32 * 4), ("sched_i1", ctypes.c_int32 * 4),
+        ("sched_mul", ctypes.c_double * 4), ("sched_div", ctypes.c_double * 4)]
 
 
 class FgxDims(ctypes.Structure):

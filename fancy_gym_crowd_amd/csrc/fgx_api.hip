@@ -110,7 +110,17 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     return fail(FGX_E_INVALID, "bad env_kind");
   if (c.rew_fct < FGX_REW_SIMPLE || c.rew_fct > FGX_REW_UNBOUNDED) return fail(FGX_E_INVALID, "Unknown reward function");
   if (c.rew_fct != FGX_REW_SIMPLE && c.env_kind != FGX_ENV_HOLE) return fail(FGX_E_INVALID, "rew_fct is a HoleReacher option");
-  if (c.learn_sub_trajectories && c.replan_period > 0)   // make_env_helpers.py:91-92
+  if (c.sched_n < 0 || c.sched_n > 4) return fail(FGX_E_INVALID, "sched_n must be in [0, 4]");
+  for (int j = 0; j < c.sched_n; ++j) {
+    const int kd = c.sched_kind[j];
+    if (kd == FGX_SCHED_EVERY && c.sched_k[j] <= 0) return fail(FGX_E_INVALID, "schedule period must be positive");
+    if (kd == FGX_SCHED_NORM_PERIOD &&
+        !(c.sched_i0[j] >= 0 && c.sched_i0[j] < c.sched_i1[j] && c.sched_i1[j] - c.sched_i0[j] <= 8 &&
+          c.sched_div[j] != 0.0))
+      return fail(FGX_E_INVALID, "norm-period clause: 0 <= i0 < i1 <= i0 + 8, div != 0");
+    if (kd < FGX_SCHED_EVERY || kd > FGX_SCHED_NORM_PERIOD) return fail(FGX_E_INVALID, "bad schedule clause kind");
+  }
+  if (c.learn_sub_trajectories && (c.replan_period > 0 || c.sched_n > 0))   // make_env_helpers.py:91-92
     return fail(FGX_E_INVALID, "Cannot used sub-trajectory learning and replanning together.");
   if (c.learn_sub_trajectories && !c.learn_tau)   // make_env_helpers.py:115-116
     return fail(FGX_E_INVALID, "learn_sub_trajectories requires learn_tau");
@@ -152,7 +162,24 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.ctrl = c.ctrl_kind;
   d.T = c.T;
   d.max_steps = c.max_episode_steps;
-  d.replan = c.replan_period;
+  // replanning schedule program (replan_period alone == one EVERY clause)
+  if (c.sched_n > 0) {
+    d.sched_n = c.sched_n;
+    for (int j = 0; j < c.sched_n; ++j) {
+      d.sched_kind[j] = c.sched_kind[j];
+      d.sched_k[j] = c.sched_k[j];
+      d.sched_i0[j] = c.sched_i0[j];
+      d.sched_i1[j] = c.sched_i1[j];
+      d.sched_mul[j] = c.sched_mul[j];
+      d.sched_div[j] = c.sched_div[j];
+      if (c.sched_kind[j] == FGX_SCHED_NORM_PERIOD) d.sched_state = 1;
+    }
+  } else if (c.replan_period > 0) {
+    d.sched_n = 1;
+    d.sched_kind[0] = SCHED_EVERY;
+    d.sched_k[0] = c.replan_period;
+  }
+  d.replan = d.sched_n > 0 ? 1 : 0;
   d.max_plans = c.max_planning_times;
   d.cond_desired = c.condition_on_desired;
   d.time_aware = c.time_aware;
@@ -160,6 +187,9 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   const int n = c.n_links;
   d.obs_dim = (c.env_kind == FGX_ENV_SIMPLE) ? 3 * n + 3 : (c.env_kind == FGX_ENV_HOLE ? 3 * n + 4 : 3 * n + 5);
   d.full_dim = d.obs_dim + (c.time_aware ? 1 : 0);
+  for (int j = 0; j < c.sched_n; ++j)
+    if (c.sched_kind[j] == FGX_SCHED_NORM_PERIOD && c.sched_i1[j] > d.full_dim)
+      return fail(FGX_E_INVALID, "norm-period clause slice exceeds the observation");
   // context mask (simple_reacher/mp_wrapper.py:32-40, hole_reacher/mp_wrapper.py:36-46,
   // viapoint_reacher/mp_wrapper.py:27-35)
   int m = 0;
@@ -186,7 +216,7 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.sub_traj = c.learn_sub_trajectories != 0;
   d.tau_lo32 = (float)c.tau_bound_lo; d.tau_hi32 = (float)c.tau_bound_hi;
   d.delay_lo32 = (float)c.delay_bound_lo; d.delay_hi32 = (float)c.delay_bound_hi;
-  const int max_s0 = c.replan_period > 0 ? c.max_episode_steps : 0;
+  const int max_s0 = (c.replan_period > 0 || c.sched_n > 0) ? c.max_episode_steps : 0;
   d.rows = max_s0 + c.T + 2;
   if (c.mp_kind == FGX_MP_PRODMP) {
     d.stride = 2 * (c.n_basis + 1) + 4;
@@ -271,7 +301,8 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_seed = off; off = align_up(off + sizeof(uint64_t) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
   // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128)
-  const bool need_rew = cfg->env_kind != FGX_ENV_SIMPLE && cfg->mp_kind != FGX_MP_NONE && h->dc.T > 128;
+  const bool need_rew = (cfg->env_kind != FGX_ENV_SIMPLE || h->dc.sched_state) && cfg->mp_kind != FGX_MP_NONE &&
+                        h->dc.T > 128;
   const size_t o_rew = off; off = align_up(off + (need_rew ? sizeof(double) * (size_t)h->dc.T * N : 0));
   e = hipMalloc(&h->state_block, off);
   if (e != hipSuccess) { delete h; return fail(FGX_E_NOMEM, std::string("hipMalloc state: ") + hipGetErrorString(e)); }

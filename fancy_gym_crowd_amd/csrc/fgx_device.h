@@ -19,6 +19,7 @@ constexpr int kMaxBasis = 16;
 
 enum : int { ENV_SIMPLE = 0, ENV_HOLE = 1, ENV_VIA = 2 };
 enum : int { REW_SIMPLE = 0, REW_VEL_ACC = 1, REW_UNBOUNDED = 2 };
+enum : int { SCHED_EVERY = 0, SCHED_AT = 1, SCHED_NORM_PERIOD = 2 };
 enum : int { MP_NONE = 0, MP_PROMP = 1, MP_DMP = 2, MP_PRODMP = 3, MP_GIVEN = 4 };
 enum : int { CTRL_PD = 0, CTRL_VEL = 1, CTRL_POS = 2 };
 
@@ -31,7 +32,7 @@ enum : int { CTRL_PD = 0, CTRL_VEL = 1, CTRL_POS = 2 };
 struct DevCfg {
   int64_t N;
   int env, nl, random_start, allow_self, allow_wall;
-  int mp, phase, nb, zs, zg, ctrl, T, max_steps, replan, max_plans, cond_desired, time_aware,
+  int mp, phase, nb, zs, zg, ctrl, T, max_steps, replan /* do_replanning */, max_plans, cond_desired, time_aware,
       return_context;
   int obs_dim;      // full env observation (3n+3 simple, 3n+4 hole)
   int full_dim;     // obs_dim + time_aware
@@ -40,6 +41,11 @@ struct DevCfg {
   int rand_width, rand_x, rand_depth;
   int rew_fct;      // HoleReacher reward function (REW_*)
   int learn_tau, learn_delay, sub_traj;   // per-env phase parameters at the front of params
+  // replanning schedule: OR of sched_n clauses (replan != 0 iff sched_n > 0); sched_state: some
+  // clause reads the observation (evaluated after every env step, no fast path)
+  int sched_n, sched_state;
+  int sched_kind[4], sched_k[4], sched_i0[4], sched_i1[4];
+  double sched_mul[4], sched_div[4];
   int rand_via, rand_target;   // ViaPointReacher: via point / target sampled at reset
   int ctx_idx[kMaxObs + 1];
   double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;

@@ -365,6 +365,83 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
   return r;
 }
 
+// ============================================================================ replanning schedule
+// Entry idx of the observation the replanning schedule receives (black_box_wrapper.py:233): the
+// env obs cast to float32, then TimeAwareObservation's t / max_episode_steps (an f64 entry).
+template <int NL>
+__device__ inline double obs_entry(const DevCfg& c, const Env<NL>& v, int idx) {
+  // register arrays are read through compile-time indices (a runtime index would move the
+  // whole env state to scratch memory)
+  if (idx < 2 * NL) {
+    const int k = idx < NL ? idx : idx - NL;
+    double qk = 0.0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) qk = (j == k) ? v.q[j] : qk;
+    double sn, cs;
+    sincos(qk, &sn, &cs);
+    return (double)(float)(idx < NL ? cs : sn);
+  }
+  if (idx < 3 * NL) {
+    double qd = 0.0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) qd = (j == idx - 2 * NL) ? v.qd[j] : qd;
+    return (double)(float)qd;
+  }
+  int p = 3 * NL;
+  if (c.env == ENV_HOLE) {
+    if (idx == p) return (double)(float)v.hw;
+    p += 1;
+  }
+  if (c.env == ENV_VIA) {
+    if (idx == p) return (double)(float)(v.jx[NL] - v.hx);
+    if (idx == p + 1) return (double)(float)(v.jy[NL] - v.hw);
+    p += 2;
+  }
+  if (idx == p) return (double)(float)(v.jx[NL] - v.gx);
+  if (idx == p + 1) return (double)(float)(v.jy[NL] - v.gy);
+  if (idx == p + 2) return (double)(float)v.steps;
+  return (double)v.steps / (double)c.max_steps;
+}
+
+// first plan sample k whose step t = steps + k + 1 satisfies a clause that depends on t only
+__device__ inline int first_static_replan(const DevCfg& c, int steps) {
+  int kr = 0x7fffffff;
+  for (int j = 0; j < c.sched_n; ++j) {
+    if (c.sched_kind[j] == SCHED_EVERY) {
+      const int P = c.sched_k[j];
+      kr = min(kr, P - 1 - (steps % P));
+    } else if (c.sched_kind[j] == SCHED_AT) {
+      const int kk = c.sched_k[j] - steps - 1;
+      if (kk >= 0) kr = min(kr, kk);
+    }
+  }
+  return kr == 0x7fffffff ? -1 : kr;
+}
+
+// t % max(int(np.linalg.norm(obs[i0:i1]) ** 2 * mul / div), 1) == 0 for any NORM_PERIOD clause
+// (crowd_navigation/utils.py:9-10); the norm is sqrt of the OpenBLAS ddot (forward fma chain)
+template <int NL>
+__device__ inline bool state_replan(const DevCfg& c, const Env<NL>& v) {
+  const int t = v.steps;
+  bool hit = false;
+  for (int j = 0; j < c.sched_n; ++j) {
+    if (c.sched_kind[j] != SCHED_NORM_PERIOD) continue;
+    double acc = 0.0;
+    for (int i = c.sched_i0[j]; i < c.sched_i1[j]; ++i) {
+      const double x = obs_entry(c, v, i);
+      acc = (i == c.sched_i0[j]) ? x * x : __builtin_fma(x, x, acc);
+    }
+    const double n = __builtin_sqrt(acc);
+    const double x = (n * n) * c.sched_mul[j] / c.sched_div[j];
+    if (!(x == x)) continue;
+    const double tr = __builtin_trunc(x);
+    if (tr > 4.0e18) continue;             // period beyond any step count
+    const long long P = tr >= 1.0 ? (long long)tr : 1;
+    hit |= ((long long)t % P) == 0;
+  }
+  return hit;
+}
+
 // ============================================================================ the BB step
 template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
 __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const float* __restrict__ params,
@@ -399,8 +476,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   plans += 1;
   // first sample index k with (k + 1 + s0) % replan == 0 (black_box_wrapper.py:233); the loop
   // stops there unless max_planning_times is exhausted, in which case it never replans again
-  const int k_replan = (c.replan > 0 && (c.max_plans <= 0 || plans < c.max_plans))
-                           ? (c.replan - 1 - (s0 % c.replan)) : -1;
+  const bool plans_ok = c.replan && (c.max_plans <= 0 || plans < c.max_plans);
+  const int k_replan = plans_ok ? first_static_replan(c, v.steps) : -1;
   PairwiseSum ps;
   ps.init();
   // plan length and the numpy pairwise split point of the return sum.  SimpleReacher never
@@ -409,12 +486,12 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   // sample (collision) and keep their step rewards in s.rew for lengths above 128.
   const int Te = (MP == MP_GIVEN && s.plan_len) ? s.plan_len[e] : c.T;
   int split = 0;
-  if (ENV == ENV_SIMPLE) {
+  if (ENV == ENV_SIMPLE && !c.sched_state) {
     int Lp = min(Te, max(1, c.max_steps - v.steps));
     if (k_replan >= 0) Lp = min(Lp, k_replan + 1);
     split = (Lp > 128) ? ((Lp / 2) & ~7) : 0;
   }
-  double* rew_row = (ENV != ENV_SIMPLE && s.rew) ? s.rew + e : nullptr;
+  double* rew_row = ((ENV != ENV_SIMPLE || c.sched_state) && s.rew) ? s.rew + e : nullptr;
   bool term = false, trunc = false, stop = false;
   float pos[NL], vel[NL];
   constexpr bool F32 = (CTRL != CTRL_PD);
@@ -471,7 +548,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
       term = (ENV != ENV_SIMPLE) ? r.coll : false;
       trunc = v.steps >= c.max_steps;
       ps.add(k, r.reward, split);
-      if (ENV != ENV_SIMPLE && rew_row) rew_row[(int64_t)k * N] = r.reward;
+      if (rew_row) rew_row[(int64_t)k * N] = r.reward;
     }
     // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
     if (LOG) {
@@ -490,7 +567,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         o.reward_ctrl[ek] = r.rctrl;
       }
     }
-    const bool replan_now = (k == k_replan);
+    bool replan_now = (k == k_replan);
+    if (J < 0 && c.sched_state && plans_ok && !replan_now) replan_now = state_replan(c, v);
     if (term || trunc || replan_now) {
       if (c.cond_desired) {
 #pragma unroll
@@ -510,6 +588,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // the blocks carry no per-lane control flow; the wave runs the blocks every lane can take.
     int lim = min(199, c.max_steps - 1) - v.steps;
     if (k_replan >= 0) lim = min(lim, k_replan);
+    if (c.sched_state) lim = 0;   // state-dependent replanning: every sample checks the schedule
     int nfast = min(Te, max(0, lim)) / 8;
     if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
     const int usplit = __builtin_amdgcn_readfirstlane(split);
@@ -532,7 +611,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     k = 8 * nfast;
   }
   while (!stop && k < Te) {
-    stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG);
+    stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG || c.sched_state);
     ++k;
   }
   const int L = k;   // samples executed (trajectory_length)
@@ -545,7 +624,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
   }
   if (ENV == ENV_SIMPLE && !LOG) v.fk();
-  o.ret[e] = (ENV != ENV_SIMPLE && L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
+  o.ret[e] = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
   o.term[e] = term;
   o.trunc[e] = trunc;
   o.tlen[e] = L;

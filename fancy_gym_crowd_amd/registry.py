@@ -152,9 +152,20 @@ register('fancy/ViaPointReacher-v0', 'via', {'n_links': 5, 'allow_self_collision
 
 
 # --------------------------------------------------------------------------- replanning schedules
-class ReplanEvery:
-    """The data-parallel form of ``replanning_schedule``: replan when the env step t % period == 0
-    (example_replanning_envs.py:37-39).  Callable with the reference's signature."""
+# ``replanning_schedule(pos, vel, obs, action, t) -> bool`` (black_box_wrapper.py:233) runs on the
+# device as a small clause program (include/fgx.h FGX_SCHED_*): the OR of up to four clauses.
+# Each class below is also a plain callable with the reference's signature, so the same object
+# can be handed to the reference's BlackBoxWrapper.
+class _Clause:
+    def clauses(self):
+        return [self]
+
+    def __or__(self, other):
+        return ReplanAny(self, other)
+
+
+class ReplanEvery(_Clause):
+    """t % period == 0 (example_replanning_envs.py:37-39, the reference's mp_wrapper schedules)."""
 
     def __init__(self, period):
         if int(period) <= 0:
@@ -164,29 +175,120 @@ class ReplanEvery:
     def __call__(self, pos, vel, obs, action, t):
         return t % self.period == 0
 
+    def batch(self, obs, t):
+        return np.asarray(t) % self.period == 0
 
-def _schedule_period(schedule, max_steps):
-    """Compile a replanning_schedule to an on-device period, or raise (only t % k == 0 is data-parallel)."""
+    def encode(self):
+        return (_lib.SCHED_EVERY, self.period, 0, 0, 0.0, 1.0)
+
+
+class ReplanAt(_Clause):
+    """t == step."""
+
+    def __init__(self, step):
+        self.step = int(step)
+
+    def __call__(self, pos, vel, obs, action, t):
+        return t == self.step
+
+    def batch(self, obs, t):
+        return np.asarray(t) == self.step
+
+    def encode(self):
+        return (_lib.SCHED_AT, self.step, 0, 0, 0.0, 1.0)
+
+
+class ReplanNormPeriod(_Clause):
+    """t % max(int(np.linalg.norm(obs[i0:i1]) ** 2 * mul / div), 1) == 0 — the state-dependent
+    period of crowd_navigation/utils.py:9-10 (obs is the time-aware observation)."""
+
+    def __init__(self, i0, i1, mul, div=1.0):
+        self.i0, self.i1, self.mul, self.div = int(i0), int(i1), float(mul), float(div)
+        if not (0 <= self.i0 < self.i1 <= self.i0 + 8) or self.div == 0.0:
+            raise ValueError("need 0 <= i0 < i1 <= i0 + 8 and div != 0")
+
+    def _period(self, o):
+        return max(int(np.linalg.norm(o[self.i0:self.i1]) ** 2 * self.mul / self.div), 1)
+
+    def __call__(self, pos, vel, obs, action, t):
+        return t % self._period(np.asarray(obs)) == 0
+
+    def batch(self, obs, t):
+        return np.array([int(ti) % self._period(o) == 0 for o, ti in zip(obs, np.asarray(t))], bool)
+
+    def encode(self):
+        return (_lib.SCHED_NORM_PERIOD, 0, self.i0, self.i1, self.mul, self.div)
+
+
+class ReplanAny(_Clause):
+    """OR of clauses (at most four on the device)."""
+
+    def __init__(self, *clauses):
+        flat = []
+        for c in clauses:
+            flat += c.clauses()
+        if not 1 <= len(flat) <= 4:
+            raise ValueError("a device schedule has 1..4 clauses")
+        self._clauses = flat
+
+    def clauses(self):
+        return list(self._clauses)
+
+    def __call__(self, pos, vel, obs, action, t):
+        return any(c(pos, vel, obs, action, t) for c in self._clauses)
+
+    def batch(self, obs, t):
+        out = np.zeros(len(np.asarray(t)), bool)
+        for c in self._clauses:
+            out |= c.batch(obs, t)
+        return out
+
+
+# crowd_navigation/utils.py:9-10 ``replan_close``
+REPLAN_CLOSE = ReplanAny(ReplanEvery(10), ReplanNormPeriod(0, 2, 10, 4))
+
+
+def _compile_schedule(schedule, max_steps):
+    """replanning_schedule -> device clause list.  Clause objects compile directly; a plain
+    callable is probed: it must be a pure function of t, of the form t % k == 0 or firing at
+    <= 4 fixed steps.  State-dependent lambdas must be written with ReplanNormPeriod."""
     if schedule is None:
-        return 0
-    if isinstance(schedule, ReplanEvery):
-        return schedule.period
-    if isinstance(schedule, int):
-        return int(schedule)
+        return []
+    if isinstance(schedule, _Clause):
+        return [c.encode() for c in schedule.clauses()]
+    if isinstance(schedule, (int, np.integer)):
+        return [ReplanEvery(int(schedule)).encode()]
     if not callable(schedule):
         raise ValueError("replanning_schedule must be callable or an int period")
     dummy = np.zeros(1)
     try:
         hits = [t for t in range(1, max_steps + 1) if bool(schedule(dummy, dummy, dummy, dummy, t))]
-        probe = [t for t in range(1, max_steps + 1) if bool(schedule(dummy + 1.0, dummy - 1.0, dummy + 2.0, dummy + 3.0, t))]
-    except Exception as e:   # state-dependent schedules (crowd_navigation/utils.py:9-10) are not data-parallel
-        raise NotImplementedError(f"replanning_schedule is not a pure function of t: {e}")
-    if hits != probe or not hits:
-        raise NotImplementedError("only schedules of the form t % k == 0 run on the device")
+        probe = [t for t in range(1, max_steps + 1)
+                 if bool(schedule(dummy + 1.0, dummy - 1.0, dummy + 2.0, dummy + 3.0, t))]
+    except Exception as e:   # state-dependent schedules (crowd_navigation/utils.py:9-10)
+        raise NotImplementedError(f"replanning_schedule is not a pure function of t ({e}); "
+                                  "express it with fgx.ReplanNormPeriod / ReplanAny")
+    if hits != probe:
+        raise NotImplementedError("state-dependent replanning_schedule: express it with "
+                                  "fgx.ReplanNormPeriod / ReplanAny")
+    if not hits:
+        return []
     k = hits[0]
-    if hits != list(range(k, max_steps + 1, k)):
-        raise NotImplementedError("only schedules of the form t % k == 0 run on the device")
-    return k
+    if hits == list(range(k, max_steps + 1, k)):
+        return [ReplanEvery(k).encode()]
+    if len(hits) <= 4:
+        return [ReplanAt(t).encode() for t in hits]
+    raise NotImplementedError("only t % k == 0, <= 4 fixed steps or fgx.Replan* clause schedules run on the device")
+
+
+def _schedule_period(schedule, max_steps):
+    """Period of a pure t % k == 0 schedule (0: none); raises for anything else."""
+    cl = _compile_schedule(schedule, max_steps)
+    if not cl:
+        return 0
+    if len(cl) == 1 and cl[0][0] == _lib.SCHED_EVERY:
+        return cl[0][1]
+    raise NotImplementedError("not a t % k == 0 schedule")
 
 
 # --------------------------------------------------------------------------- resolution
@@ -290,8 +392,10 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     action_dim = int(tg.get('action_dim', n))
     if action_dim != n:
         raise ValueError("action_dim must equal n_links for the reacher envs")
-    period = _schedule_period(bb.get('replanning_schedule'), c.max_episode_steps)
-    time_aware = (period > 0 or learn_sub or
+    sched = _compile_schedule(bb.get('replanning_schedule'), c.max_episode_steps)
+    period = sched[0][1] if (len(sched) == 1 and sched[0][0] == _lib.SCHED_EVERY) else 0
+    do_replanning = len(sched) > 0
+    time_aware = (do_replanning or learn_sub or
                   any(getattr(w, '__name__', '') == 'TimeAwareObservation' for w in wrappers))
 
     tg_type = tg.get('trajectory_generator_type', '').lower()
@@ -340,11 +444,15 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c.T = int(round(duration / c.dt))
     c.duration = float(duration)
     c.replan_period = int(period)
+    c.sched_n = len(sched)
+    for j, (kind, k, i0, i1, mul, div) in enumerate(sched):
+        c.sched_kind[j], c.sched_k[j], c.sched_i0[j], c.sched_i1[j] = kind, k, i0, i1
+        c.sched_mul[j], c.sched_div[j] = mul, div
     mpt = bb.get('max_planning_times', math.inf)
     c.max_planning_times = 0 if mpt is None or mpt == math.inf else int(mpt)
     c.condition_on_desired = int(bool(bb.get('condition_on_desired', False)))
     c.time_aware = int(time_aware)
-    c.return_context = int(not (period > 0 or learn_sub))
+    c.return_context = int(not (do_replanning or learn_sub))
     # learned phase parameters (make_env_helpers.py:115-126): bounds two env steps .. duration
     c.learn_tau, c.learn_delay, c.learn_sub_trajectories = int(learn_tau), int(learn_delay), int(learn_sub)
     tb = ph.get('tau_bound') or [c.dt * 2, duration]

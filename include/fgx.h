@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 2
+#define FGX_ABI_VERSION 3
 
 /* error codes */
 #define FGX_OK 0
@@ -59,6 +59,13 @@ extern "C" {
 #define FGX_ENV_SIMPLE 0
 #define FGX_ENV_HOLE 1
 #define FGX_ENV_VIA 2
+
+/* replanning-schedule clauses (black_box_wrapper.py:233: replanning_schedule(pos, vel, obs,
+ * action, t) with t = env steps since reset); a schedule is the OR of up to 4 clauses */
+#define FGX_SCHED_EVERY 0        /* t % k == 0            (example_replanning_envs.py:38)       */
+#define FGX_SCHED_AT 1           /* t == k                                                      */
+#define FGX_SCHED_NORM_PERIOD 2  /* t % max(int(norm(obs[i0:i1])**2 * mul / div), 1) == 0
+                                    (crowd_navigation/utils.py:9-10, obs = wrapped f64 obs)     */
 
 /* HoleReacher reward functions (hole_reacher.py:48-58, rew_fct) */
 #define FGX_REW_SIMPLE 0     /* hr_simple_reward.py        */
@@ -95,7 +102,7 @@ typedef struct fgx_config {
   int32_t ctrl_kind;            /* FGX_CTRL_*                                               */
   int32_t T;                    /* samples per plan = round(duration/dt)                    */
   int32_t max_episode_steps;    /* TimeLimit (registry max_episode_steps)                   */
-  int32_t replan_period;        /* 0 = none; else replanning_schedule: t % period == 0      */
+  int32_t replan_period;        /* 0 = none; else replanning_schedule t % period == 0 (see sched_*) */
   int32_t max_planning_times;   /* <= 0 : unlimited                                         */
   int32_t condition_on_desired; /* black_box_wrapper.py:235-237                             */
   int32_t time_aware;           /* TimeAwareObservation appended (utils/wrappers.py:49-63)  */
@@ -121,6 +128,13 @@ typedef struct fgx_config {
   double delay_bound_lo, delay_bound_hi; /* make_env_helpers.py:124-126 ([0, duration-2dt]) */
   double via_x, via_y;          /* ViaPointReacher via_target (NaN = sampled, viapoint_reacher.py:60-66) */
   double target_x, target_y;    /* ViaPointReacher target     (NaN = sampled, :68-74)      */
+  /* ---- ABI 3: replanning schedule as a clause program (sched_n == 0 and replan_period > 0
+   * is the single clause EVERY(replan_period)) */
+  int32_t sched_n;
+  int32_t sched_kind[4];        /* FGX_SCHED_*                                              */
+  int32_t sched_k[4];           /* EVERY: period; AT: step                                  */
+  int32_t sched_i0[4], sched_i1[4]; /* NORM_PERIOD: slice of the (time-aware) observation   */
+  double sched_mul[4], sched_div[4];
 } fgx_config;
 
 typedef struct fgx_dims {

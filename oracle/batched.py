@@ -290,15 +290,18 @@ class BatchedBB:
 
     def __init__(self, name, N, ctrl, mp_spec=None, traj_fn=None, replan_period=0,
                  max_planning_times=np.inf, condition_on_desired=False, info_level=0,
-                 time_aware=None, tables=None, env_kwargs=None, learned=None):
+                 time_aware=None, tables=None, env_kwargs=None, learned=None, schedule=None):
         self.env = BatchedReacher(name, N, **(env_kwargs or {}))
         self.N = N
         self.ctrl = ctrl
         self.spec = mp_spec
         self.replan = replan_period
+        self.schedule = schedule          # object with .batch(obs [N, D] f64, t [N]) -> bool [N]
+        do_replan = replan_period > 0 or schedule is not None
+        self.do_replan = do_replan
         sub = bool(learned and learned.get("sub_traj"))
-        self.time_aware = (replan_period > 0 or sub) if time_aware is None else time_aware
-        self.return_context = replan_period == 0 and not sub
+        self.time_aware = (do_replan or sub) if time_aware is None else time_aware
+        self.return_context = not do_replan and not sub
         self.max_planning_times = max_planning_times
         self.condition_on_desired = condition_on_desired
         self.info_level = info_level
@@ -311,7 +314,7 @@ class BatchedBB:
         if traj_fn is None:
             self.T = mp_spec.T
             self.tables = tables if tables is not None else mpm.build_tables(
-                mp_spec, (MAX_EPISODE_STEPS if replan_period > 0 else 0) + self.T + 2)
+                mp_spec, (MAX_EPISODE_STEPS if do_replan else 0) + self.T + 2)
             traj_fn = lambda params, s0, q, qd: mpm.trajectory(mp_spec, self.tables, params, s0, q, qd)
         self.traj_fn = traj_fn
         self.traj_steps = np.zeros(N, np.int64)
@@ -349,7 +352,7 @@ class BatchedBB:
         if self.condition_on_desired and np.any(self.has_cond):
             q_c[self.has_cond] = self.cond_pos[self.has_cond]
             qd_c[self.has_cond] = self.cond_vel[self.has_cond]
-        s0 = self.traj_steps if self.replan > 0 else np.zeros(N, np.int64)
+        s0 = self.traj_steps if self.do_replan else np.zeros(N, np.int64)
         out = self.traj_fn(params, s0, q_c, qd_c)
         pos, vel = out[0], out[1]
         T = pos.shape[1]
@@ -390,7 +393,9 @@ class BatchedBB:
             term[act] = te[act]
             trunc[act] = tr[act]
             replan_now = np.zeros(N, bool)
-            if self.replan > 0:
+            if self.schedule is not None:
+                replan_now = self.schedule.batch(o, t + 1 + self.traj_steps) & (self.plan_steps < self.max_planning_times)
+            elif self.replan > 0:
                 replan_now = ((t + 1 + self.traj_steps) % self.replan == 0) & (self.plan_steps < self.max_planning_times)
             stop = act & (te | tr | replan_now | (t + 1 >= plan_len))
             if self.condition_on_desired and np.any(stop):

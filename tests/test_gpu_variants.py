@@ -141,3 +141,43 @@ def test_bb_step_vs_oracle(ci, info_level):
                                               r_info["is_collided"][i, :L[i]])
                 np.testing.assert_array_equal(np_(info["is_success"])[i, :L[i]].astype(bool),
                                               r_info["is_success"][i, :L[i]])
+
+
+SCHED = [
+    ("fancy_ProDMP/SimpleReacher-v0", {}, lambda: fgx.REPLAN_CLOSE, 256, 10),
+    ("fancy_ProMP/LongSimpleReacher-v0", {}, lambda: fgx.ReplanAt(50) | fgx.ReplanAt(130), 128, 6),
+    ("fancy_ProMP/HoleReacher-v0", {}, lambda: fgx.ReplanEvery(40) | fgx.ReplanNormPeriod(16, 18, 30.0), 128, 6),
+    ("fancy_DMP/ViaPointReacher-v0", {}, lambda: fgx.ReplanNormPeriod(15, 17, 20.0, 1.0), 128, 6),
+]
+NAME.update({"SimpleReacher-v0": "SimpleReacher", "LongSimpleReacher-v0": "LongSimpleReacher"})
+
+
+@pytest.mark.parametrize("ci", range(len(SCHED)))
+@pytest.mark.parametrize("info_level", [0, 2])
+def test_replanning_schedule_program(ci, info_level):
+    """Generic replanning_schedule clauses on the device (fixed steps, OR, the state-dependent
+    period of crowd_navigation/utils.py:9-10) against the oracle evaluating the same callables."""
+    env_id, kw, mk, N, n_bb = SCHED[ci]
+    sched = mk()
+    env = fgx.make(env_id, num_envs=N, device=DEV, info_level=info_level, **kw,
+                   mp_config_override={"black_box_kwargs": {"replanning_schedule": sched}})
+    spec = spec_of(env)
+    okw = oracle_kwargs(env)
+    okw.pop("replan_period")
+    ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=info_level,
+                           tables=split_tables(spec, np_(env.tables())), env_kwargs=kw, schedule=sched, **okw)
+    close(np_(env.reset(seed=600)[0]), ob.reset(seed=600))
+    rng = np.random.default_rng(9)
+    lens = set()
+    for b in range(n_bb):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        lens |= set(r_info["trajectory_length"].tolist())
+        np.testing.assert_array_equal(np_(te), r_te)
+        np.testing.assert_array_equal(np_(tr), r_tr)
+        close(np_(ret), r_ret)
+        close(np_(obs), r_obs)
+        np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
+    assert len(lens) > 1

@@ -53,8 +53,8 @@ def test_library_loads_and_reports_abi():
 
 
 def test_config_struct_layout_matches_header():
-    # 20 int32, 18 doubles, then (ABI 2) 4 int32 and 8 doubles (see include/fgx.h)
-    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8
+    # 20 int32, 18 doubles, (ABI 2) 4 int32 and 8 doubles, (ABI 3) 17 int32 + pad and 8 doubles
+    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8
     assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
 
 
@@ -125,7 +125,8 @@ def test_replanning_schedule_compiles_to_period():
     assert c.replan_period == 25 and c.time_aware == 1 and c.return_context == 0
     with pytest.raises(NotImplementedError):
         fgx.resolve("fancy_ProDMP/SimpleReacher-v0",
-                    {"black_box_kwargs": {"replanning_schedule": lambda pos, vel, obs, action, t: t in (3, 50)}})
+                    {"black_box_kwargs": {"replanning_schedule":
+                                          lambda pos, vel, obs, action, t: t in (3, 50, 60, 61, 90)}})
     with pytest.raises(NotImplementedError):
         fgx.resolve("fancy_ProDMP/SimpleReacher-v0",
                     {"black_box_kwargs": {"replanning_schedule": lambda pos, vel, obs, action, t: pos[0] > 0.5}})
@@ -153,3 +154,21 @@ def test_context_space_sizes():
     # ViaPointReacher (random_start False): via - ee and goal - ee only
     from oracle import port
     assert int(port.Reacher("ViaPointReacher").context_mask().sum()) == 4
+
+
+def test_schedule_clause_compilation():
+    from fancy_gym_crowd_amd import registry
+    c, _ = fgx.resolve("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.REPLAN_CLOSE}})
+    assert c.sched_n == 2 and c.replan_period == 0 and c.time_aware == 1 and c.return_context == 0
+    assert list(c.sched_kind[:2]) == [_lib.SCHED_EVERY, _lib.SCHED_NORM_PERIOD]
+    assert (c.sched_i0[1], c.sched_i1[1], c.sched_mul[1], c.sched_div[1]) == (0, 2, 10.0, 4.0)
+    # plain lambdas firing at a few fixed steps compile to AT clauses
+    cl = registry._compile_schedule(lambda pos, vel, obs, action, t: t in (30, 120), 200)
+    assert [k[:2] for k in cl] == [(_lib.SCHED_AT, 30), (_lib.SCHED_AT, 120)]
+    # the clause objects behave like the reference's lambdas
+    obs = np.array([0.3, -0.8, 0.1])
+    ref = lambda t: t % 10 == 0 or t % max(int(np.linalg.norm(obs[:2]) ** 2 * 10 / 4), 1) == 0  # noqa: E731
+    for t in range(1, 201):
+        assert fgx.REPLAN_CLOSE(None, None, obs, None, t) == ref(t)
+    with pytest.raises(ValueError):
+        fgx.ReplanAny(*[fgx.ReplanEvery(k) for k in (2, 3, 5, 7, 11)])

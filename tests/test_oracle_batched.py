@@ -162,3 +162,32 @@ def test_batched_vs_port_learned_phase(ci):
             np.testing.assert_array_equal(inf["positions"], info["positions"][i, :L])
             if t1 or t2:
                 np.testing.assert_array_equal(p.reset(), obs[i])
+
+
+def test_batched_vs_port_state_schedule():
+    """A state-dependent replanning_schedule (crowd_navigation/utils.py:9-10 replan_close)."""
+    import fancy_gym_crowd_amd as fgx
+    spec = mp.MPSpec("prodmp", 2, 5, "exp", 1.5, alpha=10.0)
+    E = 5
+    sched = fgx.REPLAN_CLOSE
+    bb = batched.BatchedBB("SimpleReacher", E, ("pd", 1.0, 0.1), mp_spec=spec, info_level=2, schedule=sched)
+    tables = bb.tables
+    ports = []
+    for i in range(E):
+        fn = (lambda params, t0, cp, cv: tuple(
+            x[0] for x in mp.trajectory(spec, tables, params, int(round(t0 / 0.01)), cp, cv)))
+        ports.append(port.BlackBoxPort(port.Reacher("SimpleReacher"), fn, port.PD(1.0, 0.1), schedule=sched))
+    np.testing.assert_array_equal(bb.reset(seed=3), np.array([p.reset(seed=3 + i) for i, p in enumerate(ports)]))
+    rng = np.random.default_rng(5)
+    lens = set()
+    for b in range(12):
+        params = rng.standard_normal((E, spec.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = bb.step(params)
+        for i, p in enumerate(ports):
+            o, r, t1, t2, inf = p.step(params[i])
+            assert r == ret[i] and t1 == te[i] and t2 == tr[i]
+            assert inf["trajectory_length"] == info["trajectory_length"][i]
+            lens.add(inf["trajectory_length"])
+            if t1 or t2:
+                np.testing.assert_array_equal(p.reset(), obs[i])
+    assert len(lens) > 2      # the period really depends on the state
