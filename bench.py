@@ -29,6 +29,25 @@ FP64_VEC_PEAK_TF = 78.6    # MI355X FP64 vector peak (spec; half the 157.3 TF FP
 
 FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_k_episode.json")
+PMC_ISSUE = os.path.join(ROOT, "profiles", "r01_pmc_issue_k_episode.json")
+
+
+def pmc_issue(env_id, n_envs):
+    """Issue-side PMC of the metric kernel (committed rocprofv3 passes): VALUBusy and VALU
+    instructions per inner step."""
+    if env_id != WORKLOAD or n_envs != 65536:
+        return None
+    try:
+        with open(PMC_ISSUE) as f:
+            d = json.load(f)
+        c, per = d["counters_per_dispatch"], d["per_wave_sample"]
+        return {"valu_busy_pct": c["VALUBusy"], "valu_lane_util_pct": c["VALUUtilization"],
+                "valu_instr_per_inner_step_per_wave": per["SQ_INSTS_VALU"],
+                "f64_add_mul_fma_per_inner_step_per_wave": per["SQ_INSTS_VALU_ADD_F64"]
+                + per["SQ_INSTS_VALU_MUL_F64"] + per["SQ_INSTS_VALU_FMA_F64"],
+                "source": "profiles/r01_pmc_issue_k_episode.json"}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def episode_flops_per_step(env):
@@ -121,6 +140,8 @@ def main():
     ap.add_argument("--env-id", default=WORKLOAD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="launch the K steps eagerly instead of replaying them as one HIP graph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,16 +187,35 @@ def main():
     acc.zero_()
 
     K = args.steps
+    graph = None
+    if args.graph:
+        # the K BB-step launches captured once in a HIP graph (the same kernels on the same state;
+        # removes the per-launch host round trip between dependent steps)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for k in range(K):
+                    env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+            torch.cuda.synchronize()
+        except Exception as e:   # capture unsupported: time the eager launches instead
+            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            graph = None
+    acc.zero_()
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev0[k].record()
-        env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
-        ev1[k].record()
+    if graph is not None:
+        ev0[0].record()
+        graph.replay()
+        ev1[0].record()
+    else:
+        for k in range(K):
+            ev0[k].record()
+            env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+            ev1[k].record()
     if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
         all_ret = shard.gather_returns(ret.to(coll_dev))
     torch.cuda.synchronize()
@@ -183,7 +223,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     inner_local = int(acc.item())
-    kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
+    if graph is not None:   # HIP events around the replay on the launch stream: mean per BB step
+        kern_ms = ev0[0].elapsed_time(ev1[0]) / K
+    else:
+        kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
     if dist is not None:
         elapsed = shard.max_over_ranks(elapsed, coll_dev)
         inner = shard.sum_over_ranks(inner_local, coll_dev)
@@ -198,7 +241,8 @@ def main():
         valu = {"f32_tflops": f32f * steps_per_s_kernel / 1e12, "f64_tflops": f64f * steps_per_s_kernel / 1e12,
                 "peak_f32_tflops": FP32_VEC_PEAK_TF, "peak_f64_tflops": FP64_VEC_PEAK_TF,
                 "frac": f32f * steps_per_s_kernel / 1e12 / FP32_VEC_PEAK_TF
-                + f64f * steps_per_s_kernel / 1e12 / FP64_VEC_PEAK_TF}
+                + f64f * steps_per_s_kernel / 1e12 / FP64_VEC_PEAK_TF,
+                "pmc": pmc_issue(args.env_id, N)}
         bpe = episode_bytes_per_env(env)
         achieved = bpe * N / (kern_ms * 1e-3) / 1e9
         line = {
@@ -216,6 +260,7 @@ def main():
             "data": "synthetic: reset(seed=0) -> env i seeded with its global index; MP params "
                     "default_rng(1234).standard_normal((N_global, 25), f32)",
             "config": {"workload": args.env_id, "envs_per_gpu": N, "global_envs": N * world, "T": env.T,
+                       "launch": "hip graph of the K steps" if graph is not None else "eager",
                        "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"
                        + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

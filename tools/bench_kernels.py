@@ -93,6 +93,8 @@ def step_raw(env_id, N):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["episode", "traj", "raw"]
+    if "metric" in which:
+        episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
     if "episode" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
         episode("fancy_ProMP/LongSimpleReacher-v0", 262144, label="ProMP LongSimpleReacher x4 envs")

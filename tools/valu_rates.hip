@@ -30,6 +30,17 @@ __global__ __launch_bounds__(256) void k_rate(double* out, double s) {
       if (OP == 6) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(a[j]) : "v"(f[j]));
       if (OP == 7) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(f[j]) : "v"((float)c));
       if (OP == 8) asm volatile("v_mov_b64 %0, %1" : "=v"(a[j]) : "v"(a[(j + 1) & 7]));
+      if (OP == 9) asm volatile("v_fma_f64 %0, %0, 1.0, %1" : "+v"(a[j]) : "v"(c));
+      if (OP == 10) asm volatile("v_min_f64 %0, %0, %1" : "+v"(a[j]) : "v"(c));
+      if (OP == 11) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f[j]) : "v"((float)c));
+      // single dependency chain (latency): the 8 instructions all update a[0]
+      if (OP == 12) asm volatile("v_add_f64 %0, %0, %1" : "+v"(a[0]) : "v"(c));
+      if (OP == 13) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a[0]) : "v"(m), "v"(c));
+      if (OP == 15) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a[j]) : "v"(s), "v"(c));
+      if (OP == 16) asm volatile("v_add_f64 %0, %0, %1" : "+v"(a[j]) : "v"(m));
+      if (OP == 17) asm volatile("v_add_f64 %0, %0, %1" : "+v"(a[j]) : "s"(c));
+      if (OP == 18) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(a[j]) : "v"(s));
+      if (OP == 14) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[0]) : "v"((float)m), "v"((float)c));
     }
   }
   double r = 0;
@@ -66,10 +77,14 @@ static int run(const char* name, int waves_per_simd, double* d) {
 int main() {
   double* d;
   CHK(hipMalloc(&d, 64));
-  for (int w : {1, 2, 4, 8}) {
+  for (int w : {1, 4}) {
     if (run<0>("v_add_f64", w, d) || run<1>("v_mul_f64", w, d) || run<2>("v_fma_f64", w, d) ||
         run<3>("v_max_f64", w, d) || run<4>("v_fma_f32", w, d) || run<5>("v_pk_fma_f32", w, d) ||
-        run<6>("v_cvt_f64_f32", w, d) || run<7>("v_cndmask_b32", w, d) || run<8>("v_mov_b64", w, d))
+        run<6>("v_cvt_f64_f32", w, d) || run<7>("v_cndmask_b32", w, d) || run<8>("v_mov_b64", w, d) ||
+        run<9>("v_fma_f64(x,1.0,c) as add", w, d) || run<10>("v_min_f64", w, d) || run<11>("v_add_f32", w, d) ||
+        run<12>("v_add_f64 1-chain", w, d) || run<13>("v_fma_f64 1-chain", w, d) || run<14>("v_fma_f32 1-chain", w, d) ||
+        run<15>("v_fma_f64(x,one_vgpr,c)", w, d) || run<16>("v_add_f64 +0.5", w, d) ||
+        run<17>("v_add_f64 sgpr", w, d) || run<18>("v_mul_f64 x1.0", w, d))
       return 1;
   }
   CHK(hipFree(d));
