@@ -14,7 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 INC = os.path.join(HERE, "..", "include")
 LIB = os.path.join(HERE, "libfgx.so")
 OBJDIR = os.path.join(HERE, "csrc", "build")
-SOURCES = ["fgx_api.hip", "fgx_ep_simple.hip", "fgx_ep_hole.hip", "fgx_ep_via.hip"]
+SOURCES = ["fgx_ep_simple_gen.hip", "fgx_ep_hole_gen.hip", "fgx_ep_via_gen.hip", "fgx_ep_simple.hip",
+           "fgx_ep_hole.hip", "fgx_ep_via.hip", "fgx_api.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # numerics: every expression rounds like the numpy reference; fmas only where written
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",

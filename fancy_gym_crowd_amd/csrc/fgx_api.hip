@@ -58,14 +58,20 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // ------------------------------------------------------------------------ dispatch
 // The episode kernels are instantiated per env kind in their own translation units
-// (fgx_ep_simple.hip, fgx_ep_hole.hip, fgx_ep_via.hip) so that the build compiles them in parallel.
+// (fgx_ep_<env>.hip, fgx_ep_<env>_gen.hip) so that the build compiles them in parallel.
 #define FGX_FOR_NL(X) X(2) X(5)
 
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
-  if (h.dc.env == ENV_SIMPLE) return fgx_launch_episode_simple(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
-  if (h.dc.env == ENV_HOLE) return fgx_launch_episode_hole(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
-  return fgx_launch_episode_via(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
+  const bool gen = mp != MP_GIVEN && h.dc.nb != 5;   // generic basis-count instantiations
+  if (h.dc.env == ENV_SIMPLE)
+    return (gen ? fgx_launch_episode_simple_gen : fgx_launch_episode_simple)(h.dc, h.st, mp, params, dpos, dvel, o,
+                                                                           stream, g_err);
+  if (h.dc.env == ENV_HOLE)
+    return (gen ? fgx_launch_episode_hole_gen : fgx_launch_episode_hole)(h.dc, h.st, mp, params, dpos, dvel, o,
+                                                                       stream, g_err);
+  return (gen ? fgx_launch_episode_via_gen : fgx_launch_episode_via)(h.dc, h.st, mp, params, dpos, dvel, o, stream,
+                                                                     g_err);
 }
 
 static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, float* obs, hipStream_t stream) {
@@ -85,11 +91,11 @@ static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* m
 static int launch_traj_env(const Handle& h, const float* params, float* pos, float* vel, hipStream_t stream) {
   const int threads = 256;
   const int blocks = (int)((h.dc.N + threads - 1) / threads);
-#define LAUNCH(MPV, NLV)                                                                                       \
-  hipLaunchKernelGGL((k_traj_env<MPV, NLV, 5>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, params,    \
+#define LAUNCH1(MPV, NLV, NBV)                                                                           \
+  hipLaunchKernelGGL((k_traj_env<MPV, NLV, NBV>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, params, \
                      h.env_tab, pos, vel, h.plan_len)
+#define LAUNCH(MPV, NLV) do { if (h.dc.nb == 5) LAUNCH1(MPV, NLV, 5); else LAUNCH1(MPV, NLV, 0); } while (0)
   const int mp = h.dc.mp, nl = h.dc.nl;
-  if (h.dc.nb != 5) return fail(FGX_E_UNSUPPORTED, "n_basis != 5 not instantiated");
   if (mp == MP_PROMP && nl == 2) LAUNCH(MP_PROMP, 2);
   else if (mp == MP_PROMP && nl == 5) LAUNCH(MP_PROMP, 5);
   else if (mp == MP_DMP && nl == 2) LAUNCH(MP_DMP, 2);
@@ -97,6 +103,7 @@ static int launch_traj_env(const Handle& h, const float* params, float* pos, flo
   else if (mp == MP_PRODMP && nl == 2) LAUNCH(MP_PRODMP, 2);
   else if (mp == MP_PRODMP && nl == 5) LAUNCH(MP_PRODMP, 5);
   else return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+#undef LAUNCH1
 #undef LAUNCH
   HIP_TRY(hipGetLastError());
   return FGX_OK;
@@ -139,7 +146,7 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     if (c.T <= 0) return fail(FGX_E_INVALID, "T must be positive");
     // the in-register return sum restates numpy's pairwise summation with one recursion level
     if (c.T > 256) return fail(FGX_E_UNSUPPORTED, "plan length T > 256 not supported");
-    if (c.n_basis != 5) return fail(FGX_E_UNSUPPORTED, "n_basis != 5 not instantiated");
+    if (c.n_basis < 1 || c.n_basis > kGenBasis) return fail(FGX_E_UNSUPPORTED, "n_basis must be in [1, 12]");
     if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
       return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14

@@ -43,20 +43,21 @@ inline int launch_trajectory(const DevCfg& c, const DevState& s, const float* pa
   if (c.mp == MP_PROMP || c.mp == MP_PRODMP) {
     if (launch_traj_mfma(c, s, params, dpos, dvel, stream) == 0) return 0;
   }
-#define X(NL)                                                                                                     \
-  if (c.nl == NL) {                                                                                               \
-    if (c.mp == MP_PROMP)                                                                                         \
-      hipLaunchKernelGGL((k_traj_valu<MP_PROMP, NL, 5>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel); \
-    else if (c.mp == MP_DMP)                                                                                      \
-      hipLaunchKernelGGL((k_traj_valu<MP_DMP, NL, 5>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel);   \
-    else                                                                                                          \
-      hipLaunchKernelGGL((k_traj_valu<MP_PRODMP, NL, 5>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel); \
-    hipError_t e = hipGetLastError();                                                                             \
-    if (e != hipSuccess) { err = hipGetErrorString(e); return -2; }                                               \
-    return 0;                                                                                                     \
+#define LAUNCH(MPV, NLV, NBV) \
+  hipLaunchKernelGGL((k_traj_valu<MPV, NLV, NBV>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel)
+#define X(NL)                                                                                 \
+  if (c.nl == NL) {                                                                           \
+    const bool nb5 = c.nb == 5;                                                               \
+    if (c.mp == MP_PROMP) { if (nb5) LAUNCH(MP_PROMP, NL, 5); else LAUNCH(MP_PROMP, NL, 0); } \
+    else if (c.mp == MP_DMP) { if (nb5) LAUNCH(MP_DMP, NL, 5); else LAUNCH(MP_DMP, NL, 0); } \
+    else { if (nb5) LAUNCH(MP_PRODMP, NL, 5); else LAUNCH(MP_PRODMP, NL, 0); }              \
+    hipError_t e = hipGetLastError();                                                         \
+    if (e != hipSuccess) { err = hipGetErrorString(e); return -2; }                           \
+    return 0;                                                                                 \
   }
   X(2) X(5)
 #undef X
+#undef LAUNCH
   err = "n_links not instantiated (supported: 2, 5)";
   return -4;
 }

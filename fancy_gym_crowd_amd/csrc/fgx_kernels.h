@@ -99,26 +99,41 @@ __global__ __launch_bounds__(256) void k_reset(DevCfg c, DevState s, const uint6
 
 // ============================================================================ trajectories
 // Per-thread desired-trajectory generator (oracle/mp.py:trajectory), f32 throughout.
+// NB: basis functions per dof; NB = 0 is the generic instantiation with the runtime c.nb
+// (<= kGenBasis), whose chains run over compile-time slots guarded by j < nb (same fma order).
 // DIVREF: divide by tau with the IEEE division (per-env learned tau, for which the reciprocal
 // shortcut div_rcp is not verified) instead of div_rcp.
+constexpr int kGenBasis = 12;
+
 template <int MP, int NL, int NB, bool DIVREF = false>
 struct Traj {
-  static constexpr int K = (MP == MP_PRODMP) ? NB + 3 : NB;
-  float w[NL][K];          // ProMP: w ; DMP: w' ; ProDMP: [w', g', c1, c2]
+  static constexpr int NBM = NB ? NB : kGenBasis;           // weight slots per dof
+  static constexpr int K = (MP == MP_PRODMP) ? NBM + 3 : NBM;
+  float w[NL][K];          // ProMP: w ; DMP: w' ; ProDMP: [w' (NBM slots), g', c1, c2]
   float g[NL];             // DMP goal
   float y[NL], z[NL];      // DMP state
   float cur[NL], vprev[NL];// ProMP look-ahead
   const float* tab;
-  int stride, s0, T;
+  int stride, s0, T, nbr;
   float tau32, rtau32;
 
+  __device__ __forceinline__ int nb() const { return NB ? NB : nbr; }
   __device__ __forceinline__ float div_tau(float x) const { return DIVREF ? x / tau32 : div_rcp(x, tau32, rtau32); }
 
-  __device__ __forceinline__ static float chain(const float* row, const float* wd) {
+  // k-ordered f32 fma chain over the nb basis slots (== f32-input MFMA numerics)
+  __device__ __forceinline__ float chain(const float* row, const float* wd) const {
     float acc = 0.0f;
 #pragma unroll
-    for (int j = 0; j < K; ++j) acc = __builtin_fmaf(row[j], wd[j], acc);
+    for (int j = 0; j < NBM; ++j)
+      if (NB || j < nbr) acc = __builtin_fmaf(row[j], wd[j], acc);
     return acc;
+  }
+  // ProDMP: [basis (nb), goal, y1, y2] . [w', g', c1, c2]; h holds the 3 tail entries at NBM..NBM+2
+  __device__ __forceinline__ float chain3(const float* h, const float* wd) const {
+    float acc = chain(h, wd);
+    acc = __builtin_fmaf(h[NBM], wd[NBM], acc);
+    acc = __builtin_fmaf(h[NBM + 1], wd[NBM + 1], acc);
+    return __builtin_fmaf(h[NBM + 2], wd[NBM + 2], acc);
   }
 
   // params: this env's row of the [N, n_params] matrix; q0/qd0 the initial conditions
@@ -129,12 +144,13 @@ struct Traj {
   // T_ / tau32_: this plan's length and tau (learned tau, sub-trajectories)
   __device__ __forceinline__ void init(const DevCfg& c, const float* params, const float* tab_, int s0_,
                                        const double* q0, const double* qd0, int T_, float tau32_, float rtau32_) {
-    tab = tab_; stride = c.stride; s0 = s0_; T = T_; tau32 = tau32_; rtau32 = rtau32_;
+    tab = tab_; stride = c.stride; s0 = s0_; T = T_; tau32 = tau32_; rtau32 = rtau32_; nbr = c.nb;
+    const int n = nb();
     if (MP == MP_PROMP) {
 #pragma unroll
       for (int d = 0; d < NL; ++d)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) w[d][j] = params[d * NB + j];
+        for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * n + j] : 0.0f;
       const float* r1 = tab + (size_t)(s0 + 1) * stride;
 #pragma unroll
       for (int d = 0; d < NL; ++d) { cur[d] = chain(r1, w[d]); vprev[d] = 0.0f; }
@@ -142,30 +158,35 @@ struct Traj {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) w[d][j] = params[d * NB + j] * c.ws32;
-        g[d] = params[NL * NB + d] * c.gs32;
+        for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * n + j] * c.ws32 : 0.0f;
+        g[d] = params[NL * n + d] * c.gs32;
         y[d] = (float)q0[d];
         z[d] = (float)qd0[d] * tau32;
       }
     } else if (MP == MP_PRODMP) {
       const float* rb = tab + (size_t)s0 * stride;
-      const float y1 = rb[2 * NB + 2], y2 = rb[2 * NB + 3], dy1 = rb[2 * NB + 4], dy2 = rb[2 * NB + 5];
+      const float y1 = rb[2 * n + 2], y2 = rb[2 * n + 3], dy1 = rb[2 * n + 4], dy2 = rb[2 * n + 5];
       const float det = y1 * dy2 - y2 * dy1;
+      float hp[NBM + 1], hv[NBM + 1];
+#pragma unroll
+      for (int j = 0; j < NBM; ++j) {
+        hp[j] = (NB || j < n) ? rb[j] : 0.0f;
+        hv[j] = (NB || j < n) ? rb[n + 1 + j] : 0.0f;
+      }
+      hp[NBM] = rb[n];
+      hv[NBM] = rb[2 * n + 1];
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) w[d][j] = params[d * (NB + 1) + j] * c.ws32;
-        w[d][NB] = params[d * (NB + 1) + NB] * c.gs32;
-        float P = 0.0f, V = 0.0f;
-#pragma unroll
-        for (int j = 0; j <= NB; ++j) {
-          P = __builtin_fmaf(rb[j], w[d][j], P);
-          V = __builtin_fmaf(rb[NB + 1 + j], w[d][j], V);
-        }
+        for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * (n + 1) + j] * c.ws32 : 0.0f;
+        w[d][NBM] = params[d * (n + 1) + n] * c.gs32;
+        // P, V = [basis, goal] . [w', g'] (chain over nb + 1 entries)
+        float P = __builtin_fmaf(hp[NBM], w[d][NBM], chain(hp, w[d]));
+        float V = __builtin_fmaf(hv[NBM], w[d][NBM], chain(hv, w[d]));
         const float A = (float)q0[d] - P;
         const float B = (float)qd0[d] * tau32 - V;
-        w[d][NB + 1] = (dy2 * A - y2 * B) / det;
-        w[d][NB + 2] = (y1 * B - dy1 * A) / det;
+        w[d][NBM + 1] = (dy2 * A - y2 * B) / det;
+        w[d][NBM + 2] = (y1 * B - dy1 * A) / det;
       }
     }
   }
@@ -174,10 +195,11 @@ struct Traj {
   __device__ __forceinline__ void at(const DevCfg& c, int k, float* pos, float* vel) {
     const int i = s0 + k + 1;
     const float* row = tab + (size_t)i * stride;
+    const int n = nb();
     if (MP == MP_PROMP) {
       if (k < T - 1) {
         const float* nrow = row + stride;
-        const float dti = row[NB], rdt = row[NB + 1];
+        const float dti = row[n], rdt = row[n + 1];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
           const float nx = chain(nrow, w[d]);
@@ -191,7 +213,7 @@ struct Traj {
         for (int d = 0; d < NL; ++d) { pos[d] = cur[d]; vel[d] = vprev[d]; }
       }
     } else if (MP == MP_DMP) {
-      const float sdt = row[NB];
+      const float sdt = row[n];
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         pos[d] = y[d];
@@ -206,13 +228,17 @@ struct Traj {
     } else if (MP == MP_PRODMP) {
       float hp[K], hv[K];
 #pragma unroll
-      for (int j = 0; j <= NB; ++j) { hp[j] = row[j]; hv[j] = row[NB + 1 + j]; }
-      hp[NB + 1] = row[2 * NB + 2]; hp[NB + 2] = row[2 * NB + 3];
-      hv[NB + 1] = row[2 * NB + 4]; hv[NB + 2] = row[2 * NB + 5];
+      for (int j = 0; j < NBM; ++j) {
+        hp[j] = (NB || j < n) ? row[j] : 0.0f;
+        hv[j] = (NB || j < n) ? row[n + 1 + j] : 0.0f;
+      }
+      hp[NBM] = row[n]; hv[NBM] = row[2 * n + 1];
+      hp[NBM + 1] = row[2 * n + 2]; hp[NBM + 2] = row[2 * n + 3];
+      hv[NBM + 1] = row[2 * n + 4]; hv[NBM + 2] = row[2 * n + 5];
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        pos[d] = chain(hp, w[d]);
-        vel[d] = div_tau(chain(hv, w[d]));
+        pos[d] = chain3(hp, w[d]);
+        vel[d] = div_tau(chain3(hv, w[d]));
       }
     }
   }

@@ -381,3 +381,46 @@ def test_reset_mask_and_determinism():
     np.testing.assert_array_equal(after["goal"], ob.goal)
     keep = mask == 0
     np.testing.assert_array_equal(after["q"][keep], before["q"][keep])
+
+
+# ------------------------------------------------------------------------------------ basis counts
+NB_CASES = [
+    ("fancy_ProMP/LongSimpleReacher-v0", 3), ("fancy_ProMP/SimpleReacher-v0", 8),
+    ("fancy_DMP/LongSimpleReacher-v0", 10), ("fancy_ProDMP/HoleReacher-v0", 4),
+    ("fancy_ProDMP/SimpleReacher-v0", 12), ("fancy_ProMP/ViaPointReacher-v0", 7),
+]
+
+
+@pytest.mark.parametrize("ci", range(len(NB_CASES)))
+def test_generic_basis_count(ci):
+    """num_basis != 5 (mp_config_override basis_generator_kwargs) runs the generic NB
+    instantiation: trajectories bit-exact given the tables, BB steps vs the oracle."""
+    env_id, nb = NB_CASES[ci]
+    over = {"basis_generator_kwargs": {"num_basis": nb}}
+    N = 192
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+    spec = spec_of(env)
+    assert spec.n_basis == nb and env.n_params == spec.n_params
+    tabs = split_tables(spec, np_(env.tables()))
+    ref_t = oracle_tables(spec, np_(env.tables()).shape[0])
+    assert ulp_diff32(np_(env.tables())[:, :ref_t.shape[1]], ref_t).max() <= 1
+    env.reset(seed=4)
+    rng = np.random.default_rng(6)
+    params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+    st = env.get_state()
+    pos, vel = env.trajectory(torch.from_numpy(params).to(DEV))
+    rp, rv = mp.trajectory(spec, tabs, params, 0, np_(st["q"]), np_(st["qd"]))
+    np.testing.assert_array_equal(np_(pos), rp)
+    np.testing.assert_array_equal(np_(vel), rv)
+    name = env_id.split("/")[1].replace("-v0", "")
+    ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec, tables=tabs, **oracle_kwargs(env))
+    close(np_(env.reset(seed=4)[0]), ob.reset(seed=4))
+    for b in range(2):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        np.testing.assert_array_equal(np_(te), r_te)
+        assert_ulps(np_(ret), r_ret, 16)
+        close(np_(obs), r_obs)
+        np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
