@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 3
+FGX_ABI_VERSION = 4
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
 SCHED_EVERY, SCHED_AT, SCHED_NORM_PERIOD = 0, 1, 2
@@ -38,7 +38,9 @@ class FgxConfig(ctypes.Structure):
             "via_x", "via_y", "target_x", "target_y")] + [
         ("sched_n", ctypes.c_int32), ("sched_kind", ctypes.c_int32 * 4), ("sched_k", ctypes.c_int32 * 4),
         ("sched_i0", ctypes.c_int32 * 4), ("sched_i1", ctypes.c_int32 * 4),
-        ("sched_mul", ctypes.c_double * 4), ("sched_div", ctypes.c_double * 4)]
+        ("sched_mul", ctypes.c_double * 4), ("sched_div", ctypes.c_double * 4),
+        ("n_gains", ctypes.c_int32), ("reserved1", ctypes.c_int32),
+        ("p_gains", ctypes.c_double * 8), ("d_gains", ctypes.c_double * 8)]
 
 
 class FgxDims(ctypes.Structure):

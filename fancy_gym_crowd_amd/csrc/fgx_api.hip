@@ -249,8 +249,12 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.delay = c.delay;
   d.alpha_phase = c.alpha_phase;
   d.bandwidth = c.bandwidth;
-  d.p_gain = c.p_gain;
-  d.d_gain = c.d_gain;
+  if (c.n_gains != 0 && c.n_gains != c.n_links)   // p_gains * (des_pos - c_pos) must broadcast
+    return fail(FGX_E_INVALID, "per-joint PD gains must have n_links entries");
+  for (int k = 0; k < kMaxLinks; ++k) {
+    d.pg[k] = c.n_gains ? (k < c.n_links ? c.p_gains[k] : 0.0) : c.p_gain;
+    d.dg[k] = c.n_gains ? (k < c.n_links ? c.d_gains[k] : 0.0) : c.d_gain;
+  }
   d.act_lo = c.act_low;
   d.act_hi = c.act_high;
   d.act_lo32 = (float)c.act_low;

@@ -48,7 +48,8 @@ struct DevCfg {
   double sched_mul[4], sched_div[4];
   int rand_via, rand_target;   // ViaPointReacher: via point / target sampled at reset
   int ctx_idx[kMaxObs + 1];
-  double dt, rcp_dt, tau, p_gain, d_gain, act_lo, act_hi;
+  double dt, rcp_dt, tau, act_lo, act_hi;
+  double pg[kMaxLinks], dg[kMaxLinks];   // PD gains per joint (scalars broadcast)
   float act_lo32, act_hi32, dt32, rcp_dt32, tau32, rcp_tau32;
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
   double via_x0, via_y0, tgt_x0, tgt_y0;

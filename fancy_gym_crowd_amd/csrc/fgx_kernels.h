@@ -546,7 +546,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       if (CTRL == CTRL_PD) {
-        const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
+        const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
         a[d] = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
         nan_in |= (u != u);
         if (LOG || J < 0) a[d] = (u != u) ? u : a[d];
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     if (CTRL == CTRL_PD && !(LOG || J < 0) && __builtin_expect(__ballot(nan_in) != 0, 0)) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        const double u = c.p_gain * ((double)pos[d] - v.q[d]) + c.d_gain * ((double)vel[d] - v.qd[d]);
+        const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
         if (u != u) a[d] = u;
       }
     }

@@ -437,10 +437,20 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     else:
         c.alpha = float(tg.get('alpha', D['dmp_alpha']))
         c.pc_length = D['pre_compute_length_factor']
-    c.p_gain = float(ctrl.get('p_gains', 1.0))
-    c.d_gain = float(ctrl.get('d_gains', 0.5))
-    if np.ndim(ctrl.get('p_gains', 1.0)) or np.ndim(ctrl.get('d_gains', 0.5)):
-        raise NotImplementedError("per-joint PD gains")
+    # PDController(p_gains, d_gains) (pd_controller.py:16-29): scalars or one gain per joint
+    pg = np.asarray(ctrl.get('p_gains', 1), dtype=np.float64)
+    dg = np.asarray(ctrl.get('d_gains', 0.5), dtype=np.float64)
+    if pg.ndim == 0 and dg.ndim == 0:
+        c.p_gain, c.d_gain, c.n_gains = float(pg), float(dg), 0
+    else:
+        pg, dg = np.broadcast_to(pg.reshape(-1), (n,)) if pg.size in (1, n) else pg, \
+            np.broadcast_to(dg.reshape(-1), (n,)) if dg.size in (1, n) else dg
+        if pg.shape != (n,) or dg.shape != (n,):
+            raise ValueError(f"operands could not be broadcast: gains {pg.shape}/{dg.shape} for {n} joints")
+        c.n_gains = n
+        c.p_gain, c.d_gain = float(pg[0]), float(dg[0])
+        for k in range(n):
+            c.p_gains[k], c.d_gains[k] = float(pg[k]), float(dg[k])
     c.T = int(round(duration / c.dt))
     c.duration = float(duration)
     c.replan_period = int(period)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 3
+#define FGX_ABI_VERSION 4
 
 /* error codes */
 #define FGX_OK 0
@@ -135,6 +135,11 @@ typedef struct fgx_config {
   int32_t sched_k[4];           /* EVERY: period; AT: step                                  */
   int32_t sched_i0[4], sched_i1[4]; /* NORM_PERIOD: slice of the (time-aware) observation   */
   double sched_mul[4], sched_div[4];
+  /* ---- ABI 4: per-joint PD gains (pd_controller.py:16-29 with tuple gains); n_gains = 0 uses
+   * the scalars p_gain / d_gain for every joint, else n_gains == n_links */
+  int32_t n_gains;
+  int32_t reserved1;
+  double p_gains[8], d_gains[8];
 } fgx_config;
 
 typedef struct fgx_dims {

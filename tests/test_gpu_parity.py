@@ -43,6 +43,8 @@ def spec_of(env):
 
 def ctrl_of(env):
     c = env._eng.cfg
+    if c.ctrl_kind == 0 and c.n_gains:   # per-joint gains (numpy arrays broadcast like the reference)
+        return ("pd", np.array(c.p_gains[:c.n_gains]), np.array(c.d_gains[:c.n_gains]))
     return {0: ("pd", c.p_gain, c.d_gain), 1: ("vel",), 2: ("pos",)}[c.ctrl_kind]
 
 
@@ -389,6 +391,26 @@ NB_CASES = [
     ("fancy_DMP/LongSimpleReacher-v0", 10), ("fancy_ProDMP/HoleReacher-v0", 4),
     ("fancy_ProDMP/SimpleReacher-v0", 12), ("fancy_ProMP/ViaPointReacher-v0", 7),
 ]
+
+
+def test_per_joint_pd_gains():
+    """PDController with one gain per joint (tuple gains broadcast against the joint arrays)."""
+    over = {"controller_kwargs": {"p_gains": (0.5, 0.9, 1.3, 0.7, 2.0), "d_gains": [0.05, 0.1, 0.2, 0.02, 0.3]}}
+    N = 256
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, mp_config_override=over)
+    spec = spec_of(env)
+    ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
+                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+    assert ctrl_of(env)[1].shape == (5,)
+    close(np_(env.reset(seed=8)[0]), ob.reset(seed=8))
+    rng = np.random.default_rng(1)
+    for b in range(2):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        assert_ulps(np_(ret), r_ret, 16)
+        close(np_(obs), r_obs)
+        np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
 
 
 @pytest.mark.parametrize("ci", range(len(NB_CASES)))

@@ -53,8 +53,9 @@ def test_library_loads_and_reports_abi():
 
 
 def test_config_struct_layout_matches_header():
-    # 20 int32, 18 doubles, (ABI 2) 4 int32 and 8 doubles, (ABI 3) 17 int32 + pad and 8 doubles
-    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8
+    # 20 int32, 18 doubles, (ABI 2) 4 int32 and 8 doubles, (ABI 3) 17 int32 + pad and 8 doubles,
+    # (ABI 4) 2 int32 and 16 doubles
+    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8 + 2 * 4 + 16 * 8
     assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
 
 
@@ -172,3 +173,13 @@ def test_schedule_clause_compilation():
         assert fgx.REPLAN_CLOSE(None, None, obs, None, t) == ref(t)
     with pytest.raises(ValueError):
         fgx.ReplanAny(*[fgx.ReplanEvery(k) for k in (2, 3, 5, 7, 11)])
+
+
+def test_per_joint_gains_resolution():
+    c, _ = fgx.resolve("fancy_ProMP/LongSimpleReacher-v0",
+                       {"controller_kwargs": {"p_gains": (1, 2, 3, 4, 5), "d_gains": 0.1}})
+    assert c.n_gains == 5 and list(c.p_gains[:5]) == [1, 2, 3, 4, 5] and list(c.d_gains[:5]) == [0.1] * 5
+    c, _ = fgx.resolve("fancy_ProMP/LongSimpleReacher-v0")
+    assert c.n_gains == 0 and (c.p_gain, c.d_gain) == (0.6, 0.075)
+    with pytest.raises(ValueError):   # (2,) gains do not broadcast against 5 joints
+        fgx.resolve("fancy_ProMP/LongSimpleReacher-v0", {"controller_kwargs": {"p_gains": (1.0, 2.0)}})
