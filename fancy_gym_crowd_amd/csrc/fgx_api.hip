@@ -275,8 +275,6 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.gs32 = (float)c.goal_scale;
   d.alpha32 = (float)c.alpha;
   d.beta32 = (float)(c.alpha / 4);
-  for (int j = 0; j < 100; ++j) d.lin[j] = (double)j * (1.0 / 99.0);   // np.linspace(0, 1, 100)
-  d.lin[99] = 1.0;
   return FGX_OK;
 }
 

@@ -56,7 +56,6 @@ struct DevCfg {
   double delay, alpha_phase, bandwidth;   // phase / basis generator (per-env tables)
   float tau_lo32, tau_hi32, delay_lo32, delay_hi32;   // action-space bounds of tau / delay
   float ws32, gs32, alpha32, beta32;
-  double lin[100];  // np.linspace(0, 1, 100) (hole_reacher.py:311)
 };
 
 // SoA env state, owned by the handle ([k][N] for per-link arrays).
@@ -371,9 +370,11 @@ struct Env {
   }
 
   // hole_reacher.py:308-361.  Points of link k: p_j = (c_k*lin_j + jx_k, s_k*lin_j + jy_k),
-  // j = 0..99, with p_0 = joint k and p_99 = joint k+1 exactly.  p_j.y is monotone in j
-  // (rounding is monotone), so a link whose two end joints have y >= 0 has no point below the
-  // ground: only links that dip below y = 0 evaluate their 100 points.
+  // j = 0..99, with p_0 = joint k and p_99 = joint k+1 exactly.  Both coordinates are monotone
+  // in j (lin_j increases and rounding is monotone), so every atomic test (px < left, py < 0, ...)
+  // holds on a prefix or a suffix of 0..99: each is found by a 7-step binary search over the very
+  // same point expressions, and the three wall conditions become interval intersections.  A
+  // link whose two end joints have y >= 0 cannot reach below the ground and is skipped.
   __device__ __forceinline__ bool wall_collision(const DevCfg& cf) const {
     const double left = hx - hw / 2, right = hx + hw / 2, nd = -hd;
     bool hit = false;
@@ -382,13 +383,44 @@ struct Env {
       const double y0 = jy[k], y1 = jy[k + 1];
       if (y0 >= 0.0 && y1 >= 0.0 && nd <= 0.0) continue;
       const double bx = jx[k], by = jy[k], ck = c[k], sk = s[k];
-#pragma unroll 4
-      for (int j = 0; j < 100; ++j) {
-        const double px = ck * cf.lin[j] + bx;
-        const double py = sk * cf.lin[j] + by;
-        hit |= ((px < left) && (py < 0.0)) || ((px > right) && (py < 0.0)) ||
-               ((px > left) && (px < right) && (py < nd));
-      }
+      // lin_j = np.linspace(0, 1, 100)[j] = j * RN(1/99), last = 1 (computed, not loaded: the
+      // binary searches would otherwise chain dependent memory loads)
+      auto lin = [](int j) { return j == 99 ? 1.0 : (double)j * (1.0 / 99.0); };
+      auto px = [&](int j) { return ck * lin(j) + bx; };
+      auto py = [&](int j) { return sk * lin(j) + by; };
+      // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none
+      auto first = [&](auto pred) {
+        int lo = 0, hi = 100;
+#pragma unroll
+        for (int it = 0; it < 7; ++it) {
+          const int mid = (lo + hi) >> 1;
+          const bool p = lo < hi && pred(mid);
+          if (lo < hi) { if (p) hi = mid; else lo = mid + 1; }
+        }
+        return lo;
+      };
+      // {j : f(j) < t} / {j : f(j) > t} as [lo, hi) for f monotone with slope sign of `dir`
+      auto below = [&](auto f, double dir, double t, int& lo, int& hi) {
+        if (dir > 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) < t); }); }
+        else if (dir < 0.0) { lo = first([&](int j) { return f(j) < t; }); hi = 100; }
+        else { lo = 0; hi = (f(0) < t) ? 100 : 0; }   // constant (or NaN) along the link
+      };
+      auto above = [&](auto f, double dir, double t, int& lo, int& hi) {
+        if (dir > 0.0) { lo = first([&](int j) { return f(j) > t; }); hi = 100; }
+        else if (dir < 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) > t); }); }
+        else { lo = 0; hi = (f(0) > t) ? 100 : 0; }
+      };
+      int xl0, xl1, xr0, xr1, xL0, xL1, xR0, xR1, yg0, yg1, yd0, yd1;
+      below(px, ck, left, xl0, xl1);    // px < left
+      above(px, ck, right, xr0, xr1);   // px > right
+      above(px, ck, left, xL0, xL1);    // px > left
+      below(px, ck, right, xR0, xR1);   // px < right
+      below(py, sk, 0.0, yg0, yg1);     // py < 0
+      below(py, sk, nd, yd0, yd1);      // py < -depth
+      const bool c1 = max(xl0, yg0) < min(xl1, yg1);
+      const bool c2 = max(xr0, yg0) < min(xr1, yg1);
+      const bool c3 = max(max(xL0, xR0), yd0) < min(min(xL1, xR1), yd1);
+      hit |= c1 || c2 || c3;
     }
     return hit;
   }

@@ -20,10 +20,14 @@ namespace fgx {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+constexpr int kTrajWaves = 2;   // waves per workgroup (LDS tile 20.5 KB per wave: 3 groups per CU)
+
 template <int MP, int NL>
-__global__ __launch_bounds__(256) void k_traj_mfma(DevCfg c, DevState s, const float* __restrict__ params,
-                                                   float* __restrict__ dpos, float* __restrict__ dvel) {
+__global__ __launch_bounds__(64 * kTrajWaves) void k_traj_mfma(DevCfg c, DevState s, const float* __restrict__ params,
+                                                               float* __restrict__ dpos, float* __restrict__ dvel) {
   constexpr int NB = 5, K = 8;
+  constexpr int kEnvStride = 32 * NL + 4;      // dwords per env in the LDS tile (bank-spread)
+  __shared__ __attribute__((aligned(16))) float lds_stage[kTrajWaves * 32 * kEnvStride];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int j = lane & 31, h = lane >> 5;
@@ -108,48 +112,75 @@ __global__ __launch_bounds__(256) void k_traj_mfma(DevCfg c, DevState s, const f
         cq[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sidx], bco[d][sidx], cq[d], 0, 0, 0);
       }
     }
-    // ---- epilogue: lane (j, h) owns env e, rows 8g + 4h + {0..3}, g = 0..3
-    if (valid) {
+    // ---- epilogue: lane (j, h) owns env e, rows 8g + 4h + {0..3}, g = 0..3.  The tile is
+    // staged in LDS in the output layout ([env][row][dof], env stride padded to 4 mod 32
+    // dwords) and then written with coalesced 16-B stores: each env's rows of the tile are one
+    // contiguous run of rows*NL floats in [N, T, dof].
+    float* stage = lds_stage + wave * (32 * kEnvStride);
+    float vbuf[4][4 * NL];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int k0 = tb + 8 * g + 4 * h;
-        if (k0 >= T) continue;
-        float pv[4 * NL], vv[4 * NL];
+    for (int g = 0; g < 4; ++g) {
+      const int k0 = tb + 8 * g + 4 * h;
+      float pv[4 * NL];
 #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const int reg = 4 * g + r4;
-          const int k = k0 + r4;
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int reg = 4 * g + r4;
+        const int k = k0 + r4;
 #pragma unroll
-          for (int d = 0; d < NL; ++d) {
-            const float P = cp[d][reg], Q = cq[d][reg];
-            float vel;
-            if (MP == MP_PROMP) {
-              const int kc = k < T ? k : T - 1;
-              const float* dr = tab + (size_t)((kc < T - 1) ? kc + 1 : kc) * stride + NB;
-              vel = (kc < T - 1) ? div_rcp(Q - P, dr[0], dr[1]) : div_rcp(P - Q, dr[0], dr[1]);
-            } else {
-              vel = div_rcp(Q, c.tau32, c.rcp_tau32);
-            }
-            pv[r4 * NL + d] = P;
-            vv[r4 * NL + d] = vel;
+        for (int d = 0; d < NL; ++d) {
+          const float P = cp[d][reg], Q = cq[d][reg];
+          float vel;
+          if (MP == MP_PROMP) {
+            const int kc = k < T ? k : T - 1;
+            const float* dr = tab + (size_t)((kc < T - 1) ? kc + 1 : kc) * stride + NB;
+            vel = (kc < T - 1) ? div_rcp(Q - P, dr[0], dr[1]) : div_rcp(P - Q, dr[0], dr[1]);
+          } else {
+            vel = div_rcp(Q, c.tau32, c.rcp_tau32);
           }
+          pv[r4 * NL + d] = P;
+          vbuf[g][r4 * NL + d] = vel;
         }
-        const int nrow = (T - k0) < 4 ? (T - k0) : 4;
-        float* op = dpos + (e * T + k0) * NL;
-        float* ov = dvel + (e * T + k0) * NL;
-        if (nrow == 4 && ((NL * 4) % 4) == 0) {
+      }
+      float* dst = stage + j * kEnvStride + (8 * g + 4 * h) * NL;
 #pragma unroll
-          for (int q4 = 0; q4 < NL; ++q4) {
-            f32x4 x = {pv[4 * q4], pv[4 * q4 + 1], pv[4 * q4 + 2], pv[4 * q4 + 3]};
-            f32x4 y = {vv[4 * q4], vv[4 * q4 + 1], vv[4 * q4 + 2], vv[4 * q4 + 3]};
-            *reinterpret_cast<f32x4*>(op + 4 * q4) = x;
-            *reinterpret_cast<f32x4*>(ov + 4 * q4) = y;
-          }
-        } else {
-          for (int t = 0; t < nrow * NL; ++t) { op[t] = pv[t]; ov[t] = vv[t]; }
+      for (int q4 = 0; q4 < NL; ++q4)
+        *reinterpret_cast<f32x4*>(dst + 4 * q4) = f32x4{pv[4 * q4], pv[4 * q4 + 1], pv[4 * q4 + 2], pv[4 * q4 + 3]};
+    }
+    const int rows = (T - tb) < 32 ? (T - tb) : 32;     // multiple of 4 (T % 4 == 0)
+    const int chunks = rows * NL / 4;                   // 16-B chunks per env in this tile
+    const int64_t e0 = e - j;                           // first env of this wave
+    // Each wave owns its LDS tile, so a wave-local barrier suffices (LDS ops of one wave complete
+    // in order; wait for them, not for the outstanding global stores as __syncthreads would).
+    auto wave_sync = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    };
+    for (int pass = 0; pass < 2; ++pass) {
+      wave_sync();
+      if (pass == 1) {   // restage with the velocities
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float* dst = stage + j * kEnvStride + (8 * g + 4 * h) * NL;
+#pragma unroll
+          for (int q4 = 0; q4 < NL; ++q4)
+            *reinterpret_cast<f32x4*>(dst + 4 * q4) =
+                f32x4{vbuf[g][4 * q4], vbuf[g][4 * q4 + 1], vbuf[g][4 * q4 + 2], vbuf[g][4 * q4 + 3]};
+        }
+        wave_sync();
+      }
+      float* out = pass == 0 ? dpos : dvel;
+      constexpr int kFull = 32 * NL / 4;   // chunks per env of a full tile (division by a constant)
+      for (int idx = lane; idx < 32 * chunks; idx += 64) {
+        const int je = (chunks == kFull) ? idx / kFull : idx / chunks;
+        const int ch = idx - je * chunks;
+        const int64_t ee = e0 + je;
+        if (ee < N) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(stage + je * kEnvStride + 4 * ch);
+          *reinterpret_cast<f32x4*>(out + (ee * T + tb) * NL + 4 * ch) = x;
         }
       }
     }
+    wave_sync();
   }
 }
 
@@ -157,9 +188,9 @@ inline int launch_traj_mfma(const DevCfg& c, const DevState& s, const float* par
                             hipStream_t stream) {
   if (c.replan != 0 || c.nb != 5 || c.cond_desired || (c.T % 4) != 0) return 1;   // per-env plan starts: VALU kernel
   if (((uintptr_t)dpos | (uintptr_t)dvel) & 15) return 1;
-  const int threads = 256;
+  const int threads = 64 * kTrajWaves;
   const int64_t groups = (c.N + 31) / 32;
-  const int blocks = (int)((groups + 3) / 4);
+  const int blocks = (int)((groups + kTrajWaves - 1) / kTrajWaves);
 #define X(NL)                                                                                                  \
   if (c.nl == NL) {                                                                                            \
     if (c.mp == MP_PROMP)                                                                                      \

@@ -446,3 +446,32 @@ def test_generic_basis_count(ci):
         assert_ulps(np_(ret), r_ret, 16)
         close(np_(obs), r_obs)
         np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
+
+
+@pytest.mark.parametrize("name,kw", [("HoleReacher", {}), ("HoleReacher", {"hole_width": 0.3, "hole_x": 1.0}),
+                                     ("HoleReacher", {"rew_fct": "unbounded"})])
+def test_wall_collision_randomised_raw_steps(name, kw):
+    """Many random arm configurations through the step-based env: the device wall check (binary
+    searches over the monotone link points, fgx_device.h wall_collision) must flag exactly the
+    states the reference's 100-points-per-link test flags."""
+    N, steps = 2048, 60
+    env = fgx.make("fancy/HoleReacher-v0", num_envs=N, device=DEV, **kw)
+    env.reset(seed=123)
+    ob = batched.BatchedReacher(name, N, **kw)
+    ob.reset(list(range(N)), [123 + i for i in range(N)])
+    rng = np.random.default_rng(31)
+    drift = rng.uniform(-3.0, 3.0, (N, 5))
+    n_coll = 0
+    for t in range(steps):
+        a = (rng.uniform(-np.pi, np.pi, (N, 5)) + drift).astype(np.float32)
+        obs, rew, te, tr, info = env.step(torch.from_numpy(a))
+        o_r, r_r, te_r, tr_r, _ = ob.step(a.astype(np.float64), np.ones(N, bool), True)
+        np.testing.assert_array_equal(np_(te).astype(bool), te_r)
+        np.testing.assert_array_equal(np_(tr).astype(bool), tr_r)
+        close(np_(rew), r_r)
+        close(np_(info["final_observation"]), o_r)
+        n_coll += int(te_r.sum())
+        done = np.nonzero(te_r | tr_r)[0]
+        if len(done):
+            ob.reset(list(done))
+    assert n_coll > 100

@@ -17,20 +17,32 @@ dev = torch.device("cuda", 0)
 
 
 def timed(fn, reps=20, warm=3):
+    """Seconds per call: the reps calls captured in one HIP graph and replayed between two
+    events, so that host launch overhead (ctypes) does not show up as GPU time."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+    except Exception:   # not capturable: eager launches
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps * 1e-3   # seconds per call
 
 
-def episode(env_id, N, over=None, label=None, reps=20):
-    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over)
+def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
+    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over, **(env_kwargs or {}))
     env.reset(seed=0)
     P = env.n_params
     params = torch.from_numpy(np.random.default_rng(1234).standard_normal((N, P), dtype=np.float32)).to(dev)
@@ -59,10 +71,10 @@ def trajectory(env_id, N, force_valu=False):
     T, n = env.T, env.dof
     pos = torch.empty((N, T, n), device=dev)
     vel = torch.empty_like(pos)
-    lib, h, s = env._eng.lib, env._eng.h, env._eng.stream()
+    lib, h = env._eng.lib, env._eng.h
     import ctypes
     args = [ctypes.c_void_p(x.data_ptr()) for x in (params, pos, vel)]
-    t = timed(lambda: lib.fgx_trajectory(h, *args, s))
+    t = timed(lambda: lib.fgx_trajectory(h, *args, env._eng.stream()))   # current (capture) stream
     bytes_ = N * (env.n_params * 4 + 2 * T * n * 4)
     K = 8
     flops = N * n * T * 2 * 2 * K          # two K=8 GEMMs (pos + next/vel) incl. zero padding
@@ -81,9 +93,9 @@ def step_raw(env_id, N):
     te = torch.empty(N, dtype=torch.uint8, device=dev)
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     import ctypes
-    lib, h, s = env._eng.lib, env._eng.h, env._eng.stream()
+    lib, h = env._eng.lib, env._eng.h
     args = [ctypes.c_void_p(x.data_ptr()) for x in (a, obs, rew, te, tr)]
-    t = timed(lambda: lib.fgx_step_raw(h, *args, None, 1, s), reps=50)
+    t = timed(lambda: lib.fgx_step_raw(h, *args, None, 1, env._eng.stream()), reps=50)
     # algorithmic bytes per env-step: action in, state r/w, obs out, reward, flags
     state = 2 * n * 8 * 2 + 16 + 24 + 12 * 2
     b = N * (n * 4 + state + env.obs_dim * 4 + 8 + 2)
@@ -93,6 +105,22 @@ def step_raw(env_id, N):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["episode", "traj", "raw"]
+    if "bw" in which:   # what plain torch kernels reach on this box (write / copy streams)
+        for mb in (524, 2048):
+            n = mb * (1 << 20) // 4
+            a = torch.empty(n, device=dev)
+            b = torch.empty(n, device=dev)
+            t = timed(lambda: a.fill_(1.0), reps=20)
+            print(json.dumps(dict(kernel="torch fill_", MB=mb, us=t * 1e6, write_GBps=n * 4 / t / 1e9)), flush=True)
+            t = timed(lambda: b.copy_(a), reps=20)
+            print(json.dumps(dict(kernel="torch copy_", MB=mb, us=t * 1e6, GBps=2 * n * 4 / t / 1e9)), flush=True)
+            del a, b
+    if "hole" in which:   # HoleReacher cost split: full, no wall check, no self-collision check
+        episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3", reps=5)
+        episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_wall_collision", reps=5,
+                env_kwargs={"allow_wall_collision": True})
+        episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_self_collision", reps=5,
+                env_kwargs={"allow_self_collision": True})
     if "metric" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
     if "episode" in which:
