@@ -82,6 +82,39 @@ def episode_bytes_per_env(env):
     return reads + writes
 
 
+def basis_gemm(env, params, reps=10):
+    """The MP basis x weights contraction as its own launch (BlackBoxWrapper.get_trajectory ->
+    fgx_trajectory -> k_traj_mfma, v_mfma_f32_32x32x2_f32 with K = 8): time per launch from HIP
+    events around a graph replay of `reps` launches, MFMA utilisation against the f32 matrix peak
+    and the HBM rate of its [N, T, dof] f32 outputs."""
+    N, T, n = env.num_envs, env.T, env.dof
+    pos = torch.empty((N, T, n), dtype=torch.float32, device=params.device)
+    vel = torch.empty_like(pos)
+    lib, h = env._eng.lib, env._eng.h
+    import ctypes
+    args = [ctypes.c_void_p(x.data_ptr()) for x in (params, pos, vel)]
+    launch = lambda: lib.fgx_trajectory(h, *args, env._eng.stream())   # noqa: E731
+    launch()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    flops = 2 * 2 * 8 * N * n * T                 # two K = 8 GEMMs (positions, next positions)
+    out_bytes = 2 * 4 * N * T * n + 4 * N * env.n_params
+    return {"kernel": "k_traj_mfma", "us": t * 1e6, "mfma_tflops": flops / t / 1e12,
+            "peak_tflops": FP32_VEC_PEAK_TF, "mfma_frac": flops / t / 1e12 / FP32_VEC_PEAK_TF,
+            "hbm_GBps": out_bytes / t / 1e9, "hbm_frac": out_bytes / t / 1e9 / HBM_PEAK_GBS,
+            "note": "K = 8 (5 basis + zero pad): arithmetic intensity 2 flop/B, bound by the output "
+                    "write; the fused k_episode evaluates the same contraction in registers instead"}
+
+
 def cpu_baseline(seconds=12.0, cores=None):
     """The oracle port (structure-matched per-env Python loop of the reference) on host cores."""
     import multiprocessing as mp_
@@ -271,6 +304,11 @@ def main():
                                  "bound (see valu); per-substep HBM design would need 242 B/step",
                          "valu": valu},
         }
+        if world == 1 and env.T % 4 == 0:
+            try:
+                line["basis_gemm"] = basis_gemm(env, params)
+            except Exception as e:   # report, never fail the bench line on the side measurement
+                line["basis_gemm"] = {"error": str(e)}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)
