@@ -475,3 +475,55 @@ def test_wall_collision_randomised_raw_steps(name, kw):
         if len(done):
             ob.reset(list(done))
     assert n_coll > 100
+
+
+def test_set_state_then_step_matches_oracle():
+    """fgx_set_state (checkpoint restore): a BB step from an arbitrary restored state."""
+    N = 192
+    env = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=N, device=DEV)
+    env.reset(seed=17)
+    rng = np.random.default_rng(2)
+    st = {k: np_(v) for k, v in env.get_state().items()}
+    q = st["q"] + rng.uniform(-0.3, 0.3, st["q"].shape)
+    qd = rng.uniform(-1, 1, st["qd"].shape)
+    steps = rng.integers(0, 150, N).astype(np.int32)
+    env.set_state(q=q, qd=qd, steps=steps)
+    back = {k: np_(v) for k, v in env.get_state().items()}
+    np.testing.assert_array_equal(back["q"], q)
+    np.testing.assert_array_equal(back["qd"], qd)
+    np.testing.assert_array_equal(back["steps"], steps)
+    spec = spec_of(env)
+    ob = batched.BatchedBB("HoleReacher", N, ctrl_of(env), mp_spec=spec, tables=split_tables(spec, np_(env.tables())),
+                           **oracle_kwargs(env))
+    ob.reset(seed=17)
+    ob.env.q, ob.env.qd, ob.env.steps = q.copy(), qd.copy(), steps.astype(np.int64)
+    ob.env._fk()
+    params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+    obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+    r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+    np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+    np.testing.assert_array_equal(np_(te), r_te)
+    np.testing.assert_array_equal(np_(tr), r_tr)
+    assert_ulps(np_(ret), r_ret, 16)
+    close(np_(obs), r_obs)
+
+
+def test_no_autoreset_and_mean_aggregation():
+    """autoreset=False keeps finished envs (gymnasium without the VectorEnv wrapper);
+    reward_aggregation=np.mean divides the pairwise sum by the trajectory length."""
+    N = 128
+    over = {"black_box_kwargs": {"reward_aggregation": np.mean}}
+    env = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV, autoreset=False,
+                   mp_config_override=over)
+    ref = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV)
+    env.reset(seed=5)
+    ref.reset(seed=5)
+    params = torch.from_numpy(np.random.default_rng(0).standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)
+    obs, ret, te, tr, info = env.step(params)
+    obs_r, ret_r, te_r, tr_r, info_r = ref.step(params)
+    assert bool(tr.all())
+    np.testing.assert_array_equal(np_(obs), np_(info_r["final_observation"]))   # not reset
+    np.testing.assert_array_equal(np_(ret), np_(ret_r) / np_(info_r["trajectory_length"]).astype(np.float64))
+    assert bool((env.get_state()["steps"] == 200).all())
+    obs2, ret2, te2, tr2, info2 = env.step(params)   # past the TimeLimit: truncated after 1 step
+    assert bool((info2["trajectory_length"] == 1).all()) and bool(tr2.all())
