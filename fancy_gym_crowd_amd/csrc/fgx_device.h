@@ -165,10 +165,16 @@ struct PairwiseSum {
   // Unrolled fast loop: compile-time slot J == k & 7 and a block-uniform phase PH (bit 0: the
   // sample is in [0, 128), bit 1: in [split, T)).  The accumulators start at 0, so 0 + v == v
   // replaces numpy's first-block copy (only the sign of an all-zero partial sum can differ).
+  // Fast blocks are always complete, so the running tails are not needed inside them: the
+  // caller sets t = comb(a), u = comb(b) after the fast loop (sync_tails).
   template <int J, int PH>
   __device__ __forceinline__ void add_fast(double v) {
-    if (PH & 1) { a[J] = a[J] + v; t = (J == 7) ? comb(a) : t + v; }
-    if (PH & 2) { b[J] = b[J] + v; u = (J == 7) ? comb(b) : u + v; }
+    if (PH & 1) a[J] = a[J] + v;
+    if (PH & 2) b[J] = b[J] + v;
+  }
+  __device__ __forceinline__ void sync_tails() {
+    t = comb(a);
+    u = comb(b);
   }
   __device__ __forceinline__ void add(int k, double v, int split) {
     if (split > 0 && k == split) first = comb(a);   // blocks [0, split) only

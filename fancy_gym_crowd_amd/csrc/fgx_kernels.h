@@ -635,6 +635,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #undef FGX_SAMPLE
     }
     k = 8 * nfast;
+    ps.sync_tails();   // fast blocks end on complete 8-blocks: tails = combined accumulators
   }
   while (!stop && k < Te) {
     stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG || c.sched_state);
