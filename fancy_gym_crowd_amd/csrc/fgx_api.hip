@@ -88,12 +88,13 @@ static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* m
   return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
 }
 
-static int launch_traj_env(const Handle& h, const float* params, float* pos, float* vel, hipStream_t stream) {
+static int launch_traj_env(const Handle& h, const float* params, float* pos, float* vel, hipStream_t stream,
+                           float* info_pos = nullptr, float* info_vel = nullptr) {
   const int threads = 256;
   const int blocks = (int)((h.dc.N + threads - 1) / threads);
 #define LAUNCH1(MPV, NLV, NBV)                                                                           \
   hipLaunchKernelGGL((k_traj_env<MPV, NLV, NBV>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, params, \
-                     h.env_tab, pos, vel, h.plan_len)
+                     h.env_tab, pos, vel, h.plan_len, info_pos, info_vel)
 #define LAUNCH(MPV, NLV) do { if (h.dc.nb == 5) LAUNCH1(MPV, NLV, 5); else LAUNCH1(MPV, NLV, 0); } while (0)
   const int mp = h.dc.mp, nl = h.dc.nl;
   if (mp == MP_PROMP && nl == 2) LAUNCH(MP_PROMP, 2);
@@ -446,11 +447,12 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
   if (h->learned()) {
-    // per-env plans first (written straight into the info buffers when those are requested),
-    // then the episode over the given plans with per-env lengths
-    float* P = (info && info->positions) ? info->positions : h->plan_pos;
-    float* V = (info && info->velocities) ? info->velocities : h->plan_vel;
-    int rc = launch_traj_env(*h, params, P, V, (hipStream_t)stream);
+    // per-env plans first (and, when requested, the time-major info copies), then the episode
+    // over the given plans with per-env lengths
+    float* P = h->plan_pos;
+    float* V = h->plan_vel;
+    int rc = launch_traj_env(*h, params, P, V, (hipStream_t)stream, info ? info->positions : nullptr,
+                             info ? info->velocities : nullptr);
     if (rc) return rc;
     Handle hh = *h;
     hh.st.plan_len = h->plan_len;

@@ -578,7 +578,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
     // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
     if (LOG) {
-      const int64_t ek = e * c.T + k;
+      const int64_t ek = (int64_t)k * N + e;   // info arrays are time-major [T, N, ...]: coalesced
       if (o.step_actions)
         for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = a[d];
       if (o.positions && MP != MP_GIVEN)
@@ -642,12 +642,25 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     ++k;
   }
   const int L = k;   // samples executed (trajectory_length)
-  // the full desired plan is reported (black_box_wrapper.py:245-246)
-  if (LOG && o.positions && MP != MP_GIVEN) {
+  if (LOG) {
+    // the full desired plan is reported (black_box_wrapper.py:245-246); the per-step arrays end
+    // at trajectory_length: rows L..T-1 are padded with NaN (0 for the flags) in the same pass
+    const double dnan = __builtin_nan("");
+    const float fnan = __builtin_nanf("");
     for (int kk = L; kk < c.T; ++kk) {
-      tg.at(c, kk, pos, vel);
-      const int64_t ek = e * c.T + kk;
-      for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
+      const int64_t ek = (int64_t)kk * N + e;
+      if (o.positions && MP != MP_GIVEN) {
+        tg.at(c, kk, pos, vel);
+        for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
+      }
+      if (o.step_actions)
+        for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = dnan;
+      if (o.step_rewards) o.step_rewards[ek] = dnan;
+      if (o.step_obs)
+        for (int q = 0; q < c.full_dim; ++q) o.step_obs[ek * c.full_dim + q] = fnan;
+      if (o.is_collided) { o.is_collided[ek] = 0; o.is_success[ek] = 0; }
+      if (o.end_effector) { o.end_effector[ek * 2] = dnan; o.end_effector[ek * 2 + 1] = dnan; }
+      if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
     }
   }
   if (ENV == ENV_SIMPLE && !LOG) v.fk();

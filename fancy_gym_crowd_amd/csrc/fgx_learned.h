@@ -16,7 +16,8 @@ namespace fgx {
 
 template <int MP, int NL, int NB>
 __global__ __launch_bounds__(256) void k_traj_env(DevCfg c, DevState s, const float* __restrict__ params,
-                                                  float* env_tab, float* dpos, float* dvel, int32_t* plan_len) {
+                                                  float* env_tab, float* dpos, float* dvel, int32_t* plan_len,
+                                                  float* info_pos, float* info_vel) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= c.N) return;
   const int64_t N = c.N;
@@ -66,7 +67,21 @@ __global__ __launch_bounds__(256) void k_traj_env(DevCfg c, DevState s, const fl
       dpos[(e * c.T + k) * NL + d] = pos[d];
       dvel[(e * c.T + k) * NL + d] = vel[d];
     }
+    if (info_pos) {   // info['positions'/'velocities'], time-major [T, N, dof]
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        info_pos[((int64_t)k * N + e) * NL + d] = pos[d];
+        info_vel[((int64_t)k * N + e) * NL + d] = vel[d];
+      }
+    }
   }
+  if (info_pos)   // the plan ends at T_e: NaN beyond (info arrays are [T, N, dof])
+    for (int k = Te; k < c.T; ++k)
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        info_pos[((int64_t)k * N + e) * NL + d] = __builtin_nanf("");
+        info_vel[((int64_t)k * N + e) * NL + d] = __builtin_nanf("");
+      }
   if (plan_len) plan_len[e] = Te;
 }
 

@@ -148,29 +148,30 @@ class BlackBoxVectorEnv:
         return obs, {}
 
     def _info_buffers(self):
+        """verbose-2 per-step arrays.  The device writes them time-major ([T, N, ...], coalesced
+        across envs, include/fgx.h fgx_info); the caller sees [N, T, ...] transposed views."""
         if self.info_level < 2:
             return None, {}
         N, T, n, dev = self.num_envs, self.T, self.dof, self.device
-        b = dict(positions=torch.full((N, T, n), float("nan"), dtype=torch.float32, device=dev),
-                 velocities=torch.full((N, T, n), float("nan"), dtype=torch.float32, device=dev),
-                 step_actions=torch.full((N, T, n), float("nan"), dtype=torch.float64, device=dev),
-                 step_observations=torch.full((N, T, self.full_dim), float("nan"), dtype=torch.float32, device=dev),
-                 step_rewards=torch.full((N, T), float("nan"), dtype=torch.float64, device=dev))
+        # every row is written by the kernel (NaN / 0 after trajectory_length): no fill here
+        e = lambda *shape, dt=torch.float32: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
+        raw = dict(positions=e(T, N, n), velocities=e(T, N, n), step_actions=e(T, N, n, dt=torch.float64),
+                   step_observations=e(T, N, self.full_dim), step_rewards=e(T, N, dt=torch.float64))
         info = _lib.FgxInfo()
-        info.positions, info.velocities = b["positions"].data_ptr(), b["velocities"].data_ptr()
-        info.step_actions, info.step_obs = b["step_actions"].data_ptr(), b["step_observations"].data_ptr()
-        info.step_rewards = b["step_rewards"].data_ptr()
+        info.positions, info.velocities = raw["positions"].data_ptr(), raw["velocities"].data_ptr()
+        info.step_actions, info.step_obs = raw["step_actions"].data_ptr(), raw["step_observations"].data_ptr()
+        info.step_rewards = raw["step_rewards"].data_ptr()
         if self.meta["kind"] in ("hole", "via"):
-            b["is_collided"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
-            b["is_success"] = torch.zeros((N, T), dtype=torch.uint8, device=dev)
-            b["end_effector"] = torch.full((N, T, 2), float("nan"), dtype=torch.float64, device=dev)
-            info.is_collided, info.is_success = b["is_collided"].data_ptr(), b["is_success"].data_ptr()
-            info.end_effector = b["end_effector"].data_ptr()
+            raw["is_collided"] = e(T, N, dt=torch.uint8)
+            raw["is_success"] = e(T, N, dt=torch.uint8)
+            raw["end_effector"] = e(T, N, 2, dt=torch.float64)
+            info.is_collided, info.is_success = raw["is_collided"].data_ptr(), raw["is_success"].data_ptr()
+            info.end_effector = raw["end_effector"].data_ptr()
         else:
-            b["reward_dist"] = torch.full((N, T), float("nan"), dtype=torch.float64, device=dev)
-            b["reward_ctrl"] = torch.full((N, T), float("nan"), dtype=torch.float64, device=dev)
-            info.reward_dist, info.reward_ctrl = b["reward_dist"].data_ptr(), b["reward_ctrl"].data_ptr()
-        return info, b
+            raw["reward_dist"] = e(T, N, dt=torch.float64)
+            raw["reward_ctrl"] = e(T, N, dt=torch.float64)
+            info.reward_dist, info.reward_ctrl = raw["reward_dist"].data_ptr(), raw["reward_ctrl"].data_ptr()
+        return info, {k: v.transpose(0, 1) for k, v in raw.items()}
 
     def _check_actions(self, actions):
         a = torch.as_tensor(actions, device=self.device)

@@ -148,18 +148,21 @@ typedef struct fgx_dims {
 } fgx_dims;
 
 /* Optional per-step outputs of fgx_step / fgx_step_traj (black_box_wrapper.py:185-249,
- * verbose >= 2).  Any pointer may be NULL.  Steps after trajectory_length are left untouched. */
+ * verbose >= 2).  Any pointer may be NULL.  Rows after trajectory_length are set to NaN (0 for the
+ * u8 flags); positions / velocities hold the whole plan (NaN after a learned plan length).
+ * The arrays are TIME-MAJOR, [T, N, ...] (sample k of env e at row k*N + e), so that the
+ * per-step writes of neighbouring envs are coalesced; [N, T, ...] is a transposed view. */
 typedef struct fgx_info {
-  float* positions;      /* [N, T, dof]  desired positions                                 */
-  float* velocities;     /* [N, T, dof]  desired velocities                                */
-  double* step_actions;  /* [N, T, dof]  clipped controller actions                        */
-  float* step_obs;       /* [N, T, obs_dim + time_aware]  full (unmasked) observations     */
-  double* step_rewards;  /* [N, T]                                                         */
-  uint8_t* is_collided;  /* [N, T]  HoleReacher info                                       */
-  uint8_t* is_success;   /* [N, T]  HoleReacher info                                       */
-  double* end_effector;  /* [N, T, 2] HoleReacher info                                     */
-  double* reward_dist;   /* [N, T]  SimpleReacher info                                     */
-  double* reward_ctrl;   /* [N, T]  SimpleReacher info                                     */
+  float* positions;      /* [T, N, dof]  desired positions                                 */
+  float* velocities;     /* [T, N, dof]  desired velocities                                */
+  double* step_actions;  /* [T, N, dof]  clipped controller actions                        */
+  float* step_obs;       /* [T, N, obs_dim + time_aware]  full (unmasked) observations     */
+  double* step_rewards;  /* [T, N]                                                         */
+  uint8_t* is_collided;  /* [T, N]  HoleReacher / ViaPointReacher info                     */
+  uint8_t* is_success;   /* [T, N]  HoleReacher / ViaPointReacher info                     */
+  double* end_effector;  /* [T, N, 2] HoleReacher / ViaPointReacher info                   */
+  double* reward_dist;   /* [T, N]  SimpleReacher info                                     */
+  double* reward_ctrl;   /* [T, N]  SimpleReacher info                                     */
   int64_t* inner_steps;  /* [1] += sum of trajectory_length over all envs (device counter)   */
 } fgx_info;
 

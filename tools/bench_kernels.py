@@ -121,6 +121,24 @@ if __name__ == "__main__":
                 env_kwargs={"allow_wall_collision": True})
         episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_self_collision", reps=5,
                 env_kwargs={"allow_self_collision": True})
+    if "log" in which:   # info_level=2 (verbose 2 per-step arrays) through the public step()
+        for env_id in ("fancy_ProMP/LongSimpleReacher-v0", "fancy_ProDMP/HoleReacher-v0"):
+            env = fgx.make(env_id, num_envs=65536, device=dev, info_level=2)
+            env.reset(seed=0)
+            params = torch.randn((65536, env.n_params), device=dev)
+            for _ in range(2):
+                env.step(params)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                env.step(params)
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps(dict(kernel="step(info_level=2)", config=env_id, envs=65536,
+                                  us_per_step=e0.elapsed_time(e1) / 5 * 1e3)), flush=True)
+            del env
+            torch.cuda.empty_cache()
     if "metric" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
     if "episode" in which:
