@@ -34,7 +34,7 @@ def make(env_id, num_envs=1, device="cuda", mp_config_override=None, **kwargs):
 
 
 def __getattr__(name):
-    if name in ("BlackBoxVectorEnv", "StepVectorEnv", "Box"):
+    if name in ("BlackBoxVectorEnv", "StepVectorEnv", "Box", "ResetNeeded"):
         from . import vector_env
         return getattr(vector_env, name)
     raise AttributeError(name)

@@ -79,6 +79,15 @@ class _Engine:
             pass
 
 
+class ResetNeeded(RuntimeError):
+    """step() before reset() (gymnasium's OrderEnforcing wrapper, error.ResetNeeded [EXT-M])."""
+
+
+def _order_check(env):
+    if env._needs_reset:
+        raise ResetNeeded("Cannot call env.step() before calling env.reset()")
+
+
 class BlackBoxVectorEnv:
     """N black-box envs (one BB step = one whole (sub-)episode) on one GPU."""
 
@@ -92,6 +101,7 @@ class BlackBoxVectorEnv:
         self.info_level = meta["verbose"] if info_level is None else int(info_level)
         self.autoreset = bool(autoreset)
         self.seed_offset = int(seed_offset)
+        self._needs_reset = True
         self._eng = _Engine(cfg, num_envs, device)
         d = self._eng.dims
         self.dof, self.T, self.n_params = d.dof, d.T, d.n_params
@@ -145,6 +155,7 @@ class BlackBoxVectorEnv:
         if options and options.get("reset_mask") is not None:
             mask = torch.as_tensor(options["reset_mask"], dtype=torch.uint8, device=self.device).contiguous()
         _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), _ptr(mask), _ptr(obs), self._eng.stream()))
+        self._needs_reset = False
         return obs, {}
 
     def _info_buffers(self):
@@ -182,6 +193,7 @@ class BlackBoxVectorEnv:
         return a.contiguous()
 
     def step(self, actions):
+        _order_check(self)
         a = self._check_actions(actions)
         N = self.num_envs
         obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
@@ -198,6 +210,7 @@ class BlackBoxVectorEnv:
 
     def step_trajectory(self, des_pos, des_vel):
         """BB step with caller-supplied desired trajectories [N, T, dof] f32 (no MP evaluation)."""
+        _order_check(self)
         N, T, n = self.num_envs, self.T, self.dof
         p = torch.as_tensor(des_pos, device=self.device).to(torch.float32).contiguous()
         v = torch.as_tensor(des_vel, device=self.device).to(torch.float32).contiguous()
@@ -243,8 +256,9 @@ class BlackBoxVectorEnv:
 
     # ------------------------------------------------------------------ fast path (bench)
     def step_into(self, actions, obs, ret, te, tr, tl, fobs=None, inner_steps=None):
-        """Allocation-free BB step into preallocated buffers (no checks; for benchmarks).
+        """Allocation-free BB step into preallocated buffers (no argument checks; for benchmarks).
         inner_steps: optional int64 [1] device counter += sum of trajectory lengths."""
+        _order_check(self)
         info = None
         if inner_steps is not None:
             info = _lib.FgxInfo()
@@ -297,6 +311,7 @@ class StepVectorEnv:
         self.num_envs = int(num_envs)
         self.autoreset = bool(autoreset)
         self.seed_offset = int(seed_offset)
+        self._needs_reset = True
         self._eng = _Engine(cfg, num_envs, device)
         d = self._eng.dims
         self.dof, self.obs_dim = d.dof, d.obs_dim
@@ -311,9 +326,11 @@ class StepVectorEnv:
         if seed is not None:
             seeds = (torch.arange(N, dtype=torch.int64, device=self.device) + (int(seed) + self.seed_offset)).contiguous()
         _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), None, _ptr(obs), self._eng.stream()))
+        self._needs_reset = False
         return obs, {}
 
     def step(self, actions):
+        _order_check(self)
         a = torch.as_tensor(actions, device=self.device).to(torch.float32).contiguous()
         N = self.num_envs
         if tuple(a.shape) != (N, self.dof):

@@ -527,3 +527,15 @@ def test_no_autoreset_and_mean_aggregation():
     assert bool((env.get_state()["steps"] == 200).all())
     obs2, ret2, te2, tr2, info2 = env.step(params)   # past the TimeLimit: truncated after 1 step
     assert bool((info2["trajectory_length"] == 1).all()) and bool(tr2.all())
+
+
+def test_step_before_reset_raises():
+    """gymnasium's OrderEnforcing: step() before reset() raises ResetNeeded."""
+    env = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=8, device=DEV)
+    with pytest.raises(fgx.ResetNeeded):
+        env.step(torch.zeros((8, env.n_params)))
+    env.reset(seed=0)
+    env.step(torch.zeros((8, env.n_params)))
+    raw = fgx.make("fancy/SimpleReacher-v0", num_envs=8, device=DEV)
+    with pytest.raises(fgx.ResetNeeded):
+        raw.step(torch.zeros((8, 2)))
