@@ -81,11 +81,13 @@ class FgxError(RuntimeError):
     pass
 
 
-def load(path=LIB_PATH):
-    """Load libfgx.so and declare every exported symbol (no GPU needed)."""
+def load(path=None):
+    """Load libfgx.so and declare every exported symbol (no GPU needed).  FGX_LIB names another
+    build of the same ABI (kernel experiments, tools/exp); the default is the in-tree library."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("FGX_LIB") or LIB_PATH
     import torch  # noqa: F401  (bind to torch's HIP runtime, see module docstring)
     if not os.path.exists(path):
         raise FgxError(f"libfgx.so not built ({path}); run __graft_entry__.build() — there is no CPU fallback")

@@ -334,6 +334,7 @@ struct Env {
   __device__ __forceinline__ void reset(const DevCfg& cf, Pcg64& r, bool seeded, uint64_t seed) {
     if (cf.env != ENV_HOLE) {
       const bool via = (cf.env == ENV_VIA);
+      if (!via) { hx = 0.0; hw = 0.0; hd = 0.0; }   // unused by SimpleReacher: keep the state defined
       if (seeded) {
         pcg_seed(r, seed);
         first_joint(cf, r);

@@ -113,11 +113,15 @@ struct Traj {
   float g[NL];             // DMP goal
   float y[NL], z[NL];      // DMP state
   float cur[NL], vprev[NL];// ProMP look-ahead
-  const float* tab;
-  int stride, s0, T, nbr;
+  const float* tab;        // row s0 of the basis table: plan sample k reads rows k + 1, k + 2
+  int stride, T, nbr;
   float tau32, rtau32;
+  // table row stride, compile-time for a fixed basis count (build_devcfg in fgx_api.hip): every
+  // row address of an unrolled sample block is then a constant offset from one base
+  static constexpr int KS = NB ? ((MP == MP_PRODMP) ? 2 * (NB + 1) + 4 : (NB + 2 + 3) & ~3) : 0;
 
   __device__ __forceinline__ int nb() const { return NB ? NB : nbr; }
+  __device__ __forceinline__ int str() const { return KS ? KS : stride; }
   __device__ __forceinline__ float div_tau(float x) const { return DIVREF ? x / tau32 : div_rcp(x, tau32, rtau32); }
 
   // k-ordered f32 fma chain over the nb basis slots (== f32-input MFMA numerics)
@@ -141,17 +145,21 @@ struct Traj {
                                        const double* q0, const double* qd0) {
     init(c, params, tab_, s0_, q0, qd0, c.T, c.tau32, c.rcp_tau32);
   }
-  // T_ / tau32_: this plan's length and tau (learned tau, sub-trajectories)
+  // T_ / tau32_: this plan's length and tau (learned tau, sub-trajectories).  goff: offset of the
+  // DMP goal entries in params (default NL * nb; the per-joint generators of k_episode_jp pass
+  // params + d * nb and the offset of goal d, c.nl * nb + d - d * nb).
   __device__ __forceinline__ void init(const DevCfg& c, const float* params, const float* tab_, int s0_,
-                                       const double* q0, const double* qd0, int T_, float tau32_, float rtau32_) {
-    tab = tab_; stride = c.stride; s0 = s0_; T = T_; tau32 = tau32_; rtau32 = rtau32_; nbr = c.nb;
+                                       const double* q0, const double* qd0, int T_, float tau32_, float rtau32_,
+                                       int goff = -1) {
+    stride = c.stride; T = T_; tau32 = tau32_; rtau32 = rtau32_; nbr = c.nb;
+    tab = tab_ + (size_t)s0_ * str();
     const int n = nb();
     if (MP == MP_PROMP) {
 #pragma unroll
       for (int d = 0; d < NL; ++d)
 #pragma unroll
         for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * n + j] : 0.0f;
-      const float* r1 = tab + (size_t)(s0 + 1) * stride;
+      const float* r1 = tab + str();
 #pragma unroll
       for (int d = 0; d < NL; ++d) { cur[d] = chain(r1, w[d]); vprev[d] = 0.0f; }
     } else if (MP == MP_DMP) {
@@ -159,12 +167,12 @@ struct Traj {
       for (int d = 0; d < NL; ++d) {
 #pragma unroll
         for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * n + j] * c.ws32 : 0.0f;
-        g[d] = params[NL * n + d] * c.gs32;
+        g[d] = params[(goff < 0 ? NL * n : goff) + d] * c.gs32;
         y[d] = (float)q0[d];
         z[d] = (float)qd0[d] * tau32;
       }
     } else if (MP == MP_PRODMP) {
-      const float* rb = tab + (size_t)s0 * stride;
+      const float* rb = tab;
       const float y1 = rb[2 * n + 2], y2 = rb[2 * n + 3], dy1 = rb[2 * n + 4], dy2 = rb[2 * n + 5];
       const float det = y1 * dy2 - y2 * dy1;
       float hp[NBM + 1], hv[NBM + 1];
@@ -191,14 +199,15 @@ struct Traj {
     }
   }
 
-  // desired (pos, vel) of plan sample k (row i = s0 + k + 1); call with k = 0, 1, 2, ...
+  // desired (pos, vel) of plan sample k (row s0 + k + 1); call with k = 0, 1, 2, ...
+  // MID: the caller guarantees k < T - 1 (no last-sample branch)
+  template <bool MID = false>
   __device__ __forceinline__ void at(const DevCfg& c, int k, float* pos, float* vel) {
-    const int i = s0 + k + 1;
-    const float* row = tab + (size_t)i * stride;
+    const float* row = tab + (size_t)(k + 1) * str();
     const int n = nb();
     if (MP == MP_PROMP) {
-      if (k < T - 1) {
-        const float* nrow = row + stride;
+      if (MID || k < T - 1) {
+        const float* nrow = row + str();
         const float dti = row[n], rdt = row[n + 1];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
@@ -218,7 +227,7 @@ struct Traj {
       for (int d = 0; d < NL; ++d) {
         pos[d] = y[d];
         vel[d] = div_tau(z[d]);
-        if (k < T - 1) {
+        if (MID || k < T - 1) {
           const float f = chain(row, w[d]);
           const float acc = c.alpha32 * (c.beta32 * (g[d] - y[d]) - z[d]) + f;
           z[d] = z[d] + sdt * acc;
@@ -468,6 +477,44 @@ __device__ inline bool state_replan(const DevCfg& c, const Env<NL>& v) {
   return hit;
 }
 
+// BB-step outputs, VectorEnv auto-reset and state write-back of one env (black_box_wrapper.py:
+// 241-253; gymnasium SyncVectorEnv autoreset), shared by k_episode and k_episode_jp.  v holds
+// the env after its last sample with FK refreshed.
+template <int NL>
+__device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState& s, const Outputs& o, int64_t e,
+                                                 Env<NL>& v, int plans, int L, double ret, bool term, bool trunc) {
+  const int64_t N = c.N;
+  o.ret[e] = ret;
+  o.term[e] = term;
+  o.trunc[e] = trunc;
+  o.tlen[e] = L;
+  if (o.inner_steps) {   // wave-reduce the trajectory lengths, one atomic per (full) wave
+    if (__ballot(1) == ~0ull) {
+      long long sum = L;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+      if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
+    } else {
+      atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)L);
+    }
+  }
+  float* ob = o.obs + e * c.out_dim;
+  float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
+  if (o.autoreset && (term || trunc)) {
+    if (fo) emit_obs(c, v, c.return_context, fo, nullptr);
+    Pcg64 rg = load_rng(s.rng, N, e);
+    v.reset(c, rg, false, 0);
+    store_rng(s.rng, N, e, rg);
+    plans = 0;
+    v.flags = 0;
+    emit_obs(c, v, c.return_context, ob, nullptr);
+  } else {
+    emit_obs(c, v, c.return_context, ob, fo);
+  }
+  store_env(c, s, e, v);
+  s.plans[e] = plans;
+}
+
 // ============================================================================ the BB step
 template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
 __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const float* __restrict__ params,
@@ -664,35 +711,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
   }
   if (ENV == ENV_SIMPLE && !LOG) v.fk();
-  o.ret[e] = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
-  o.term[e] = term;
-  o.trunc[e] = trunc;
-  o.tlen[e] = L;
-  if (o.inner_steps) {   // wave-reduce the trajectory lengths, one atomic per (full) wave
-    if (__ballot(1) == ~0ull) {
-      long long sum = L;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-      if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
-    } else {
-      atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)L);
-    }
-  }
-  float* ob = o.obs + e * c.out_dim;
-  float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
-  if (o.autoreset && (term || trunc)) {
-    if (fo) emit_obs(c, v, c.return_context, fo, nullptr);
-    Pcg64 rg = load_rng(s.rng, N, e);
-    v.reset(c, rg, false, 0);
-    store_rng(s.rng, N, e, rg);
-    plans = 0;
-    v.flags = 0;
-    emit_obs(c, v, c.return_context, ob, nullptr);
-  } else {
-    emit_obs(c, v, c.return_context, ob, fo);
-  }
-  store_env(c, s, e, v);
-  s.plans[e] = plans;
+  const double ret = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
+  episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
 }
 
 // ============================================================================ step-based

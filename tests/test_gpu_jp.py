@@ -1,0 +1,131 @@
+"""k_episode_jp (fgx_jp.h, one wave per joint) against k_episode (one env per lane) and the oracle.
+
+The joint-parallel kernel serves SimpleReacher + PD with shared basis tables at info_level 0.
+FGX_EPISODE_KERNEL=jp / =classic force either kernel for the same call, so every output and
+the whole device state must agree bit for bit between the two kernels, for partial workgroups
+(N % 64 != 0), lanes at different env steps / replanning phases, NaN parameters, per-joint gains
+and condition_on_desired; the oracle checks the jp results independently.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import fancy_gym_crowd_amd as fgx
+from oracle import batched
+
+from test_gpu_parity import DEV, assert_ulps, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("fancy_ProMP/LongSimpleReacher-v0", None, 1000, 3),
+    ("fancy_ProMP/SimpleReacher-v0", None, 130, 3),
+    ("fancy_DMP/LongSimpleReacher-v0", None, 333, 2),
+    ("fancy_DMP/SimpleReacher-v0", None, 64, 2),
+    ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}, 200, 10),
+    ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25),
+                                                            "condition_on_desired": True}}, 256, 10),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(150)}}, 128, 4),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanAt(3)}}, 96, 3),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"controller_kwargs": {"p_gains": (0.5, 0.9, 1.3, 0.7, 2.0),
+                                                                "d_gains": [0.05, 0.1, 0.2, 0.02, 0.3]}}, 256, 2),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"basis_generator_kwargs": {"num_basis": 7}}, 192, 2),
+]
+
+
+def _state(env):
+    return {k: np_(v).copy() for k, v in env.get_state().items()}
+
+
+def _run(env_id, over, N, n_bb, kernel, seed, params_seq, set_state=None, mask_after_first=True):
+    """kernel: "jp" (k_episode_jp wherever it applies) or "classic" (k_episode)."""
+    old = os.environ.get("FGX_EPISODE_KERNEL")
+    os.environ["FGX_EPISODE_KERNEL"] = kernel
+    try:
+        env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+        out = [np_(env.reset(seed=seed)[0])]
+        if set_state is not None:
+            env.set_state(**set_state)
+        for b in range(n_bb):
+            obs, ret, te, tr, info = env.step(torch.from_numpy(params_seq[b]).to(DEV))
+            out += [np_(obs), np_(ret), np_(te), np_(tr), np_(info["trajectory_length"]),
+                    np_(info["final_observation"])]
+            out += list(_state(env).values())
+            if b == 0 and mask_after_first:
+                mask = np.zeros(N, np.uint8)
+                mask[::3] = 1
+                out.append(np_(env.reset(options={"reset_mask": torch.from_numpy(mask)})[0]))
+        return out
+    finally:
+        if old is None:
+            os.environ.pop("FGX_EPISODE_KERNEL", None)
+        else:
+            os.environ["FGX_EPISODE_KERNEL"] = old
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert x.shape == y.shape and x.dtype == y.dtype, i
+        # NaN-aware bitwise equality
+        np.testing.assert_array_equal(x.view(np.uint8), y.view(np.uint8), err_msg=f"output {i}")
+
+
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_jp_equals_classic_kernel(ci):
+    env_id, over, N, n_bb = CASES[ci]
+    probe = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+    rng = np.random.default_rng(40 + ci)
+    params = [rng.standard_normal((N, probe.n_params), dtype=np.float32) for _ in range(n_bb)]
+    _same(_run(env_id, over, N, n_bb, "jp", 300 + ci, params),
+          _run(env_id, over, N, n_bb, "classic", 300 + ci, params))
+
+
+def test_jp_equals_classic_nan_and_restored_steps():
+    """NaN / inf / huge parameters (np.clip NaN propagation, clip at the torque bound) and a
+    restored state with every env at a different step (segments of every length 1..200)."""
+    env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 320
+    probe = fgx.make(env_id, num_envs=N, device=DEV)
+    rng = np.random.default_rng(5)
+    p = rng.standard_normal((2, N, probe.n_params)).astype(np.float32)
+    p[0, 3, 4] = np.nan
+    p[0, 70, 0] = np.inf
+    p[0, 130, :] = 3e4
+    p[1, 200, 7] = -np.inf
+    probe.reset(seed=9)
+    st = _state(probe)
+    steps = (np.arange(N) * 7 % 200).astype(np.int32)
+    qd = rng.uniform(-2, 2, st["qd"].shape)
+    ss = dict(q=st["q"], qd=qd, steps=steps)
+    a = _run(env_id, None, N, 2, "jp", 9, list(p), set_state=ss, mask_after_first=False)
+    b = _run(env_id, None, N, 2, "classic", 9, list(p), set_state=ss, mask_after_first=False)
+    _same(a, b)
+    assert np.isnan(a[2][3]) and np.isfinite(a[2][5])   # the NaN env's return is NaN
+
+
+def test_jp_vs_oracle_desynchronised():
+    """jp alone (selected by default at this size) against the oracle with lanes at different env
+    steps (set_state)."""
+    env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 200
+    env = fgx.make(env_id, num_envs=N, device=DEV)
+    spec = spec_of(env)
+    ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
+                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+    env.reset(seed=21)
+    ob.reset(seed=21)
+    steps = (np.arange(N) % 200).astype(np.int32)
+    env.set_state(steps=steps)
+    ob.env.steps = steps.astype(np.int64)
+    rng = np.random.default_rng(8)
+    for b in range(2):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        np.testing.assert_array_equal(np_(tr), r_tr)
+        assert_ulps(np_(ret), r_ret, 16)
+        close(np_(obs), r_obs)
+        np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
+        np.testing.assert_array_equal(np_(env.get_state()["steps"]), ob.env.steps)

@@ -139,6 +139,21 @@ if __name__ == "__main__":
                                   us_per_step=e0.elapsed_time(e1) / 5 * 1e3)), flush=True)
             del env
             torch.cuda.empty_cache()
+    if "scan" in which:   # metric env over the envs-per-GPU axis (occupancy / tail effects)
+        for n in (4096, 8192, 16384, 32768, 49152, 65536, 81920, 98304, 131072, 262144):
+            episode("fancy_ProMP/LongSimpleReacher-v0", n, label="scan: ProMP LongSimpleReacher", reps=10)
+        for n in (16384, 32768, 65536, 131072):
+            episode("fancy_DMP/LongSimpleReacher-v0", n, label="scan: DMP LongSimpleReacher", reps=10)
+    if "scanmp" in which:   # every MP kind and link count over the envs-per-GPU axis
+        rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
+        for env_id, over in (("fancy_ProDMP/LongSimpleReacher-v0", None), ("fancy_ProMP/SimpleReacher-v0", None),
+                             ("fancy_DMP/SimpleReacher-v0", None), ("fancy_ProDMP/SimpleReacher-v0", None),
+                             ("fancy_ProDMP/SimpleReacher-v0", rp)):
+            for n in (4096, 16384, 32768, 49152, 65536, 131072):
+                episode(env_id, n, over=over, label="scan: " + env_id + (" replan25" if over else ""), reps=10)
+    if "scanlite" in which:
+        for n in (16384, 32768, 49152, 65536, 131072):
+            episode("fancy_ProMP/LongSimpleReacher-v0", n, label="scan: ProMP LongSimpleReacher", reps=10)
     if "metric" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
     if "episode" in which:
