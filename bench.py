@@ -298,7 +298,7 @@ def main():
                        + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.env_id, N),
-                         "kernel": "k_episode", "kernel_ms": kern_ms, "bytes_per_env": bpe,
+                         "kernel": env.episode_kernel(), "kernel_ms": kern_ms, "bytes_per_env": bpe,
                          "bytes_per_inner_step": bpe * N / (inner_local / K),
                          "note": "state lives in registers for all T substeps: the kernel is VALU-issue "
                                  "bound (see valu); per-substep HBM design would need 242 B/step",

@@ -72,7 +72,9 @@ EXPORTS = {
     "fgx_get_state": (ctypes.c_int, [ctypes.c_void_p] * 7),
     "fgx_set_state": (ctypes.c_int, [ctypes.c_void_p] * 7),
     "fgx_get_tables": (ctypes.c_int, [ctypes.c_void_p] * 3),
+    "fgx_episode_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
 }
+EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws"}
 
 _LIB = None
 
@@ -83,7 +85,7 @@ class FgxError(RuntimeError):
 
 def load(path=None):
     """Load libfgx.so and declare every exported symbol (no GPU needed).  FGX_LIB names another
-    build of the same ABI (kernel experiments, tools/exp); the default is the in-tree library."""
+    build of the same ABI (kernel experiments); the default is the in-tree library."""
     global _LIB
     if _LIB is not None:
         return _LIB

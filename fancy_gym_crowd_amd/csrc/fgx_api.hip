@@ -537,4 +537,11 @@ int fgx_get_tables(void* handle, float* out, void* stream) {
   return FGX_OK;
 }
 
+int fgx_episode_kernel(void* handle, int32_t info_level) {
+  Handle* h = (Handle*)handle;
+  if (!h) return fail(FGX_E_INVALID, "null handle");
+  const int mp = h->learned() ? MP_GIVEN : h->dc.mp;
+  return episode_kernel_choice(h->dc, mp, info_level >= 2, h->learned());
+}
+
 }  // extern "C"

@@ -6,7 +6,7 @@
 #include <cstring>
 #include <string>
 
-#include "fgx_jp.h"
+#include "fgx_ws.h"
 
 // returns 0 / FGX_E_* code, message in err
 #define FGX_DECLARE_LAUNCH(NAME)                                                                             \
@@ -22,36 +22,53 @@ FGX_DECLARE_LAUNCH(fgx_launch_episode_via_gen)
 
 namespace fgx {
 
-// k_episode_jp (fgx_jp.h) covers SimpleReacher + PD over the shared basis tables with static
-// replanning schedules, max_episode_steps <= 200 and no per-step info.  FGX_EPISODE_KERNEL=classic
-// forces k_episode, =jp forces k_episode_jp wherever it applies (A/B benchmarks and the
-// kernel-equivalence tests).
-inline bool jp_enabled() {
-  const char* v = std::getenv("FGX_EPISODE_KERNEL");
-  return !(v && std::strcmp(v, "classic") == 0);
-}
+// Episode kernels: k_episode (fgx_kernels.h, one env per lane, every case), k_episode_jp (fgx_jp.h,
+// one wave per joint) and k_episode_ws (fgx_ws.h, trajectory-producer / dynamics-consumer wave
+// pairs).  The last two serve SimpleReacher + PD over the shared basis tables with static
+// replanning schedules, max_episode_steps <= 200 and no per-step info, bit-identically to
+// k_episode (tests/test_gpu_jp.py, tests/test_gpu_ws.py).  Which one runs follows the measured
+// table profiles/r01_jp_vs_classic.jsonl + profiles/r01_ws_scan.jsonl (every kernel forced over
+// envs per GPU x MP kind x links on one MI355X):
+//  * k_episode holds one wave (64 envs) per SIMD, so it takes ceil(N / (64 x 4 x CUs)) rounds of a
+//    near-fixed ~75-93 us (5 links): a lone wave issues only every ~6-9 cycles.
+//  * k_episode_jp grows ~linearly with N (5 links: ~1.65 us per 1k envs): it wins for 5 links while
+//    k_episode's single round is at most 3/4 full or its last round at most half full, and for
+//    DMP at every size (up to 2.7x).  Short replanning segments pay its per-chunk exchange.
+//  * k_episode_ws wins for 2-link ProDMP up to one full round (~10%, also with replanning).
+// FGX_EPISODE_KERNEL=classic|jp|ws forces a kernel wherever it applies (A/B benchmarks, tests).
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2 };
 
-// Where k_episode_jp beats k_episode (both kernels timed over envs per GPU x MP kind x links,
-// profiles/r01_jp_vs_classic.jsonl).  k_episode holds one wave (64 envs) per SIMD, so it runs in
-// ceil(N / (64 x 4 x CUs)) rounds of a fixed ~75-93 us; k_episode_jp's time grows ~linearly
-// (5 links: ~1.65 us per 1k envs).  Hence for 5 links: jp while k_episode's one round is at most 3/4
-// full or its last round at most half full, and DMP at every size (its per-joint Euler plan splits
-// cheaply).  Two links (2 waves per 64 envs) and short replanning segments (per-chunk exchange
-// overhead) stay on k_episode except DMP up to one full round.
-inline bool jp_preferred(const DevCfg& c, int mp) {
-  const char* v = std::getenv("FGX_EPISODE_KERNEL");
-  if (v && std::strcmp(v, "jp") == 0) return true;
-  if (c.replan) return false;
-  static const int64_t round_envs = [] {
+inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
+  static const int64_t r = [] {
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
     return (int64_t)cus * 4 * 64;
   }();
-  const int64_t tail = c.N % round_envs;
-  if (c.nl == 5)
-    return mp == MP_DMP || 4 * c.N <= 3 * round_envs || (c.N > round_envs && tail != 0 && 2 * tail <= round_envs);
-  return mp == MP_DMP && c.N <= round_envs;
+  return r;
+}
+
+inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env_plans) {
+  const bool eligible = c.env == ENV_SIMPLE && mp != MP_GIVEN && mp != MP_NONE && c.ctrl == CTRL_PD && !log &&
+                        !c.sched_state && c.T <= 256 && c.max_steps <= 200 && !per_env_plans && !c.learn_tau &&
+                        !c.learn_delay && (c.nl == 2 || c.nl == 5);
+  if (!eligible) return EK_CLASSIC;
+  if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
+    if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
+    if (std::strcmp(v, "jp") == 0) return EK_JP;
+    if (std::strcmp(v, "ws") == 0) return EK_WS;
+  }
+  const int64_t R = round_envs(), tail = c.N % R;
+  if (c.nl == 5) {
+    if (c.replan) return EK_CLASSIC;
+    if (mp == MP_DMP) return EK_JP;
+    const bool jp = 4 * c.N <= 3 * R || (c.N > R && tail != 0 && 2 * tail <= R);
+    return jp ? EK_JP : EK_CLASSIC;
+  }
+  if (mp == MP_PRODMP && c.N <= R) return EK_WS;
+  if (mp == MP_DMP && !c.replan && c.N <= R) return EK_JP;
+  return EK_CLASSIC;
 }
 
 template <int MP, int NL, int NB>
@@ -75,6 +92,28 @@ static int launch_jp(const DevCfg& c, const DevState& s, const float* params, co
   return 0;
 }
 
+template <int MP, int NL, int NB>
+static int launch_ws(const DevCfg& c, const DevState& s, const float* params, const Outputs& o, hipStream_t stream,
+                     std::string& err) {
+  const size_t lw = ws_lds_bytes<NL>(c.rows, c.stride);
+  if (lw > 160 * 1024) {
+    err = "k_episode_ws: basis table too large for LDS";
+    return -4;
+  }
+  if (lw > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)k_episode_ws<MP, NL, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lw) != hipSuccess) {
+    err = "k_episode_ws: cannot raise the dynamic LDS limit";
+    return -2;
+  }
+  const int64_t per_block = 64 * kWsPairs;
+  hipLaunchKernelGGL((k_episode_ws<MP, NL, NB>), dim3((unsigned)((c.N + per_block - 1) / per_block)), dim3(512), lw,
+                     stream, c, s, params, o);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { err = std::string("k_episode_ws launch: ") + hipGetErrorString(e); return -2; }
+  return 0;
+}
+
 template <int ENV, int MP, int CTRL, int NL, int NB>
 static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* params, const float* dpos,
                              const float* dvel, const Outputs& o, hipStream_t stream, std::string& err) {
@@ -90,9 +129,9 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     }
   }
   if constexpr (ENV == ENV_SIMPLE && MP != MP_GIVEN && CTRL == CTRL_PD) {
-    if (!log && !c.sched_state && c.T <= 256 && c.max_steps <= 200 && !s.plan_len && !c.learn_tau && !c.learn_delay &&
-        jp_enabled() && jp_preferred(c, MP))
-      return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
+    const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
+    if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
+    if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
   }
   if (log)
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), lds, stream, c, s,

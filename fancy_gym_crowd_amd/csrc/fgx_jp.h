@@ -26,7 +26,7 @@
 //
 // Every expression rounds exactly as in k_episode / the numpy reference (same operations, same
 // order); it serves ENV_SIMPLE + PD + shared tables + info_level < 2 + max_episode_steps <= 200,
-// and fgx_dispatch.h picks it over k_episode where it is measured faster (jp_preferred).
+// and fgx_dispatch.h picks it over k_episode where it is measured faster (episode_kernel_choice).
 #pragma once
 #include "fgx_kernels.h"
 

@@ -290,6 +290,15 @@ class BlackBoxVectorEnv:
         _lib.check(self._eng.lib.fgx_set_state(self._eng.h, _ptr(q), _ptr(qd), _ptr(goal), _ptr(hole), _ptr(steps),
                                                self._eng.stream()))
 
+    def episode_kernel(self, info_level=None):
+        """Name of the HIP kernel step() launches (fgx_episode_kernel): k_episode, k_episode_jp or
+        k_episode_ws; all three produce bit-identical results."""
+        lvl = self.info_level if info_level is None else int(info_level)
+        k = self._eng.lib.fgx_episode_kernel(self._eng.h, lvl)
+        if k < 0:
+            _lib.check(k)
+        return _lib.EPISODE_KERNELS[k]
+
     def tables(self):
         d = self._eng.dims
         out = torch.empty((d.table_rows, d.table_stride), dtype=torch.float32, device=self.device)

@@ -23,6 +23,7 @@
  *   fgx_get_state /   env.unwrapped.current_pos/current_vel, goal, hole black_box/raw_interface_wrapper.py:24-44
  *   fgx_set_state     (checkpoint/test access)
  *   fgx_get_tables    basis tables (test/introspection)
+ *   fgx_episode_kernel which episode kernel fgx_step launches (introspection / benchmarks)
  *
  * Conventions
  *   - Every array argument is a CALLER-OWNED DEVICE pointer (e.g. torch tensor storage) on the
@@ -213,6 +214,12 @@ int fgx_set_state(void* handle, const double* q, const double* qd, const double*
 
 /* Copy the f32 basis tables [table_rows, table_stride] to out (device). */
 int fgx_get_tables(void* handle, float* out, void* stream);
+
+/* The kernel fgx_step launches for this handle with the given info level (>= 2: per-step info
+ * arrays): 0 = k_episode (one env per lane), 1 = k_episode_jp (one wave per joint),
+ * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs); negative on error.
+ * All three give bit-identical results; the choice follows measured speed (fgx_dispatch.h). */
+int fgx_episode_kernel(void* handle, int32_t info_level);
 
 #ifdef __cplusplus
 }

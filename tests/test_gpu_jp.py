@@ -56,7 +56,8 @@ def _run(env_id, over, N, n_bb, kernel, seed, params_seq, set_state=None, mask_a
             if b == 0 and mask_after_first:
                 mask = np.zeros(N, np.uint8)
                 mask[::3] = 1
-                out.append(np_(env.reset(options={"reset_mask": torch.from_numpy(mask)})[0]))
+                # rows of envs not reset are left untouched (uninitialised): compare the reset rows
+                out.append(np_(env.reset(options={"reset_mask": torch.from_numpy(mask)})[0])[mask == 1])
         return out
     finally:
         if old is None:
@@ -66,10 +67,15 @@ def _run(env_id, over, N, n_bb, kernel, seed, params_seq, set_state=None, mask_a
 
 
 def _same(a, b):
+    """bitwise equality, except that NaN payload / sign bits are not compared (IEEE leaves them
+    unspecified; numpy and the two kernels' instruction selections need not agree on them)"""
     assert len(a) == len(b)
     for i, (x, y) in enumerate(zip(a, b)):
         assert x.shape == y.shape and x.dtype == y.dtype, i
-        # NaN-aware bitwise equality
+        if x.dtype.kind == "f":
+            nx, ny = np.isnan(x), np.isnan(y)
+            np.testing.assert_array_equal(nx, ny, err_msg=f"output {i}: NaN positions")
+            x, y = x[~nx], y[~ny]
         np.testing.assert_array_equal(x.view(np.uint8), y.view(np.uint8), err_msg=f"output {i}")
 
 

@@ -58,7 +58,7 @@ def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
     env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
     torch.cuda.synchronize()
     inner = int(acc.item())
-    print(json.dumps(dict(kernel="k_episode", config=label or env_id, envs=N, kernel_us=t * 1e6,
+    print(json.dumps(dict(kernel=env.episode_kernel(), config=label or env_id, envs=N, kernel_us=t * 1e6,
                           inner_steps_per_call=inner, inner_steps_per_s=inner / t,
                           mean_traj_len=inner / N)), flush=True)
 
