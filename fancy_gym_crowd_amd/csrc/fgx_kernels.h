@@ -604,8 +604,10 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         a[d] = (double)a32[d];
       }
     }
-    // np.clip propagates NaN; max/min do not: fix up (rare, wave-uniform branch)
-    if (CTRL == CTRL_PD && !(LOG || J < 0) && __builtin_expect(__ballot(nan_in) != 0, 0)) {
+    // np.clip propagates NaN; max/min do not: fix up (rare, wave-uniform branch).  ProMP fast
+    // blocks run only in NaN-free waves (see nan_free below): no check there.
+    if (CTRL == CTRL_PD && !(LOG || J < 0) && !(MP == MP_PROMP && J >= 0) &&
+        __builtin_expect(__ballot(nan_in) != 0, 0)) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
         const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
@@ -664,6 +666,21 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     if (c.sched_state) lim = 0;   // state-dependent replanning: every sample checks the schedule
     int nfast = min(Te, max(0, lim)) / 8;
     if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
+    if (MP == MP_PROMP && CTRL == CTRL_PD) {
+      // NaN-free waves: the PD control u is finite for every sample when the weights are finite
+      // with |w| < 1e30 (|pos| <= 5 max|phi w|, |vel| <= 2 |pos| / dt stay far inside f32), the
+      // gains are finite and |q|, |qd| < 1e300 (200 Euler steps with |a| <= 1000 cannot overflow);
+      // the fast blocks then skip np.clip's NaN fix-up, other waves take the exact generic path
+      bool ok = true;
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        ok = ok && __builtin_fabs(v.q[d]) < 1e300 && __builtin_fabs(v.qd[d]) < 1e300 &&
+             __builtin_fabs(c.pg[d]) < 1e300 && __builtin_fabs(c.dg[d]) < 1e300;
+#pragma unroll
+        for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.w[d][j]) < 1e30f;
+      }
+      if (__ballot(!ok) != 0) nfast = 0;
+    }
     const int usplit = __builtin_amdgcn_readfirstlane(split);
     if (__ballot(split != usplit) != 0) nfast = 0;   // the block phases need one split per wave
 #pragma unroll
