@@ -583,6 +583,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         pos[d] = dpos[(e * c.T + k) * NL + d];
         vel[d] = dvel[(e * c.T + k) * NL + d];
       }
+    } else if constexpr (J >= 0) {
+      tg.template at<true>(c, k, pos, vel);   // fast blocks end before the plan's last sample
     } else {
       tg.at(c, k, pos, vel);
     }
@@ -664,7 +666,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     int lim = min(199, c.max_steps - 1) - v.steps;
     if (k_replan >= 0) lim = min(lim, k_replan);
     if (c.sched_state) lim = 0;   // state-dependent replanning: every sample checks the schedule
-    int nfast = min(Te, max(0, lim)) / 8;
+    int nfast = min(Te - 1, max(0, lim)) / 8;   // (sample Te - 1 ends the plan: generic path)
     if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
     if (MP == MP_PROMP && CTRL == CTRL_PD) {
       // NaN-free waves: the PD control u is finite for every sample when the weights are finite
