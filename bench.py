@@ -28,6 +28,11 @@ FP64_VEC_PEAK_TF = 78.6    # MI355X FP64 vector peak (spec; half the 157.3 TF FP
 
 
 FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
+CLOCK_GHZ = 2.4            # MI355X peak engine clock
+# cycles per VALU instruction a single wave sustains with 8 independent f64 fma chains, and the
+# SIMD with >= 4 waves (profiles/r01_valu_rates.jsonl): k_episode runs one wave per SIMD
+SINGLE_WAVE_CYCLES = 6.12
+SIMD_CYCLES = 4.68
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_k_episode.json")
 PMC_ISSUE = os.path.join(ROOT, "profiles", "r01_pmc_issue_k_episode.json")
 
@@ -276,6 +281,16 @@ def main():
                 "frac": f32f * steps_per_s_kernel / 1e12 / FP32_VEC_PEAK_TF
                 + f64f * steps_per_s_kernel / 1e12 / FP64_VEC_PEAK_TF,
                 "pmc": pmc_issue(args.env_id, N)}
+        if valu["pmc"] is not None:   # issue rate: VALU instructions per SIMD over the kernel time
+            instr = valu["pmc"]["valu_instr_per_inner_step_per_wave"] * (inner_local / K) / 64.0
+            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+            cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9 / (instr / simds)
+            valu["issue"] = {"cycles_per_valu_instr_per_simd": cyc,
+                             "single_wave_floor_cycles": SINGLE_WAVE_CYCLES, "simd_floor_cycles": SIMD_CYCLES,
+                             "frac_of_single_wave_issue": SINGLE_WAVE_CYCLES / cyc,
+                             "frac_of_simd_issue": SIMD_CYCLES / cyc,
+                             "note": "one wave (64 envs) per SIMD at 65536 envs: the single-wave issue rate "
+                                     "is the ceiling (DESIGN.md 4.3)"}
         bpe = episode_bytes_per_env(env)
         achieved = bpe * N / (kern_ms * 1e-3) / 1e9
         line = {
