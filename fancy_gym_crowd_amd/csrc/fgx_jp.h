@@ -240,7 +240,7 @@ __global__ __launch_bounds__(NL * 64, 5) void k_episode_jp(DevCfg c, DevState s,
 
   // ---- wave 0: return and epilogue
   Env<NL> v;
-  load_env(c, s, e, v);
+  load_env(c, s, e, v, false);   // SimpleReacher: no hole / reward state
 #pragma unroll
   for (int k = 0; k < NL; ++k) { v.q[k] = qs[k * 64 + lane]; v.qd[k] = qs[(NL + k) * 64 + lane]; }
   v.steps = sg.steps + sg.L;

@@ -56,12 +56,23 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
 }
 
 // ============================================================================ state I/O
+// hole: the hole / via-point / reward-state arrays take part (SimpleReacher never reads or changes
+// them — k_reset zeroes them — so its episode kernels neither load nor store them: no registers
+// held across the sample loop for them)
 template <int NL>
-__device__ __forceinline__ void load_env(const DevCfg& c, const DevState& s, int64_t e, Env<NL>& v) {
+__device__ __forceinline__ void load_env(const DevCfg& c, const DevState& s, int64_t e, Env<NL>& v,
+                                         bool hole = true) {
   const int64_t N = c.N;
 #pragma unroll
   for (int k = 0; k < NL; ++k) { v.q[k] = s.q[k * N + e]; v.qd[k] = s.qd[k * N + e]; }
   v.gx = s.goal[e]; v.gy = s.goal[N + e];
+  v.ex = v.ey = v.cd = 0.0;
+  if (!hole) {
+    v.hx = v.hw = v.hd = 0.0;
+    v.steps = s.steps[e];
+    v.flags = s.flags[e];
+    return;
+  }
   v.hx = s.hole[e]; v.hw = s.hole[N + e]; v.hd = s.hole[2 * N + e];
   if (c.env == ENV_HOLE && c.rew_fct != REW_SIMPLE) { v.ex = s.aux[e]; v.ey = s.aux[N + e]; v.cd = s.aux[2 * N + e]; }
   v.steps = s.steps[e];
@@ -69,11 +80,17 @@ __device__ __forceinline__ void load_env(const DevCfg& c, const DevState& s, int
 }
 
 template <int NL>
-__device__ __forceinline__ void store_env(const DevCfg& c, const DevState& s, int64_t e, const Env<NL>& v) {
+__device__ __forceinline__ void store_env(const DevCfg& c, const DevState& s, int64_t e, const Env<NL>& v,
+                                          bool hole = true) {
   const int64_t N = c.N;
 #pragma unroll
   for (int k = 0; k < NL; ++k) { s.q[k * N + e] = v.q[k]; s.qd[k * N + e] = v.qd[k]; }
   s.goal[e] = v.gx; s.goal[N + e] = v.gy;
+  if (!hole) {
+    s.steps[e] = v.steps;
+    s.flags[e] = v.flags;
+    return;
+  }
   s.hole[e] = v.hx; s.hole[N + e] = v.hw; s.hole[2 * N + e] = v.hd;
   if (c.env == ENV_HOLE && c.rew_fct != REW_SIMPLE) { s.aux[e] = v.ex; s.aux[N + e] = v.ey; s.aux[2 * N + e] = v.cd; }
   s.steps[e] = v.steps;
@@ -511,7 +528,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   } else {
     emit_obs(c, v, c.return_context, ob, fo);
   }
-  store_env(c, s, e, v);
+  store_env(c, s, e, v, c.env != ENV_SIMPLE);
   s.plans[e] = plans;
 }
 
@@ -531,7 +548,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   const int64_t N = c.N;
 
   Env<NL> v;
-  load_env(c, s, e, v);
+  load_env(c, s, e, v, ENV != ENV_SIMPLE);
   int plans = s.plans[e];
   const int s0 = c.replan ? v.steps : 0;       // init_time = current_traj_steps * dt if replanning
 

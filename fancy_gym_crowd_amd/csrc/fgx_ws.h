@@ -108,7 +108,7 @@ __global__ __launch_bounds__(512, FGX_WS_WAVES) void k_episode_ws(DevCfg c, DevS
 
   // -------------------------------------------------------------------- consumer waves
   Env<NL> v;
-  load_env(c, s, e, v);
+  load_env(c, s, e, v, false);   // SimpleReacher: no hole / reward state
   const int k_replan = sg.k_replan;
   const int Te = c.T;
   // numpy pairwise split of the return sum (SimpleReacher never terminates: L is known now)
