@@ -705,18 +705,24 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nfast = min(nfast, __shfl_xor(nfast, off, 64));
     nfast = __builtin_amdgcn_readfirstlane(nfast);
-    for (int kb = 0; kb < 8 * nfast; kb += 8) {
-      if (usplit > 0 && kb == usplit) ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
-      // phase of this block (uniform): pushes into the level-1 and/or second-half sums
-      const int ph = (kb < 128 ? 1 : 0) | ((usplit > 0 && kb >= usplit) ? 2 : 0);
+    // Two loops: blocks before the pairwise split push into the level-1 sums a[] only, blocks from
+    // the split on into the second-half sums b[] only.  (With a split, L > 128 and the result is
+    // first + u: a[] and t are dead after the split, so numpy's level-1 adds there are skipped;
+    // without one every block is < L <= 128 and in the first loop.)  Each loop keeps one set of 8
+    // accumulators live.
 #define FGX_SAMPLE(J, PH) sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}, false);
 #define FGX_BLOCK(PH) \
       FGX_SAMPLE(0, PH) FGX_SAMPLE(1, PH) FGX_SAMPLE(2, PH) FGX_SAMPLE(3, PH) \
       FGX_SAMPLE(4, PH) FGX_SAMPLE(5, PH) FGX_SAMPLE(6, PH) FGX_SAMPLE(7, PH)
-      if (ph == 1) { FGX_BLOCK(1) } else if (ph == 3) { FGX_BLOCK(3) } else { FGX_BLOCK(2) }
+    const int nA = usplit > 0 ? min(nfast, usplit / 8) : nfast;
+    int kb = 0;
+    for (; kb < 8 * nA; kb += 8) { FGX_BLOCK(1) }
+    if (usplit > 0 && nfast > nA) {
+      ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
+      for (; kb < 8 * nfast; kb += 8) { FGX_BLOCK(2) }
+    }
 #undef FGX_BLOCK
 #undef FGX_SAMPLE
-    }
     k = 8 * nfast;
     ps.sync_tails();   // fast blocks end on complete 8-blocks: tails = combined accumulators
   }
