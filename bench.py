@@ -81,7 +81,8 @@ def pmc_traffic(env_id, n_envs):
 def episode_bytes_per_env(env):
     """Algorithmic HBM bytes of one k_episode launch per env (info_level 0, autoreset on)."""
     n, P, out = env.dof, env.n_params, env.out_dim
-    state = 2 * n * 8 + 2 * 8 + 3 * 8 + 3 * 4 + 5 * 8      # q, qd, goal, hole, steps/plans/flags, rng
+    hole = 0 if env._eng.cfg.env_kind == 0 else 3 * 8      # SimpleReacher kernels skip hole / aux
+    state = 2 * n * 8 + 2 * 8 + hole + 3 * 4 + 5 * 8       # q, qd, goal, [hole], steps/plans/flags, rng
     reads = P * 4 + state
     writes = state + 2 * out * 4 + 8 + 1 + 1 + 4           # state, obs, final_obs, ret, term, trunc, len
     return reads + writes
