@@ -100,6 +100,18 @@ struct Outputs {
   int autoreset;
 };
 
+// ------------------------------------------------------------------ wave reductions (all 64 lanes active)
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off, 64));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+
 // ------------------------------------------------------------------ exact small helpers
 __device__ __forceinline__ double np_max(double x, double lo) { return (x != x) ? x : (x > lo ? x : lo); }
 __device__ __forceinline__ double np_min(double x, double hi) { return (x != x) ? x : (x < hi ? x : hi); }
@@ -171,6 +183,13 @@ struct PairwiseSum {
   __device__ __forceinline__ void add_fast(double v) {
     if (PH & 1) a[J] = a[J] + v;
     if (PH & 2) b[J] = b[J] + v;
+  }
+  // A partial block (fewer than 8 samples, slots J < 7, after sync_tails): the running tail
+  // follows each push as numpy's sequential remainder would (push() with j != 7).
+  template <int J, int PH>
+  __device__ __forceinline__ void add_partial(double v) {
+    if (PH & 1) { a[J] = a[J] + v; t = t + v; }
+    if (PH & 2) { b[J] = b[J] + v; u = u + v; }
   }
   __device__ __forceinline__ void sync_tails() {
     t = comb(a);

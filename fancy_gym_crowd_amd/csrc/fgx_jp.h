@@ -46,16 +46,6 @@ inline size_t jp_lds_bytes(int rows, int stride) {
   return (size_t)(jp_ex_rows<NL>() + 2 * NL) * 64 * sizeof(double) + (size_t)rows * stride * sizeof(float);
 }
 
-__device__ __forceinline__ int wave_min(int x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off, 64));
-  return __builtin_amdgcn_readfirstlane(x);
-}
-__device__ __forceinline__ int wave_max(int x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
-  return __builtin_amdgcn_readfirstlane(x);
-}
 
 // v_max_f64 / v_min_f64 (IEEE maxNum / minNum: a NaN u gives a bound, see the chunk redo); asm so
 // that the bounds are not re-canonicalised for every sample

@@ -636,7 +636,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // ---- env.step
     const StepOut r = substep<ENV, F32, NL, (J < 0)>(c, v, a, a32, fk_always);
     if constexpr (J >= 0) {   // fast blocks: no termination, truncation or replanning inside
-      ps.template add_fast<J, PH>(r.reward);
+      if constexpr ((PH & 4) != 0) ps.template add_partial<J, (PH & 3)>(r.reward);   // partial block
+      else ps.template add_fast<J, PH>(r.reward);
       return false;
     } else {
       term = (ENV != ENV_SIMPLE) ? r.coll : false;
@@ -683,8 +684,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     int lim = min(199, c.max_steps - 1) - v.steps;
     if (k_replan >= 0) lim = min(lim, k_replan);
     if (c.sched_state) lim = 0;   // state-dependent replanning: every sample checks the schedule
-    int nfast = min(Te - 1, max(0, lim)) / 8;   // (sample Te - 1 ends the plan: generic path)
-    if (__ballot(1) != ~0ull) nfast = 0;   // partial wave (N % 64 != 0): generic path only
+    const int lim2 = min(Te - 1, max(0, lim));   // fast samples k < lim2 (sample Te - 1 ends the plan)
+    bool fast_ok = __ballot(1) == ~0ull;   // partial wave (N % 64 != 0): generic path only
     if (MP == MP_PROMP && CTRL == CTRL_PD) {
       // NaN-free waves: the PD control u is finite for every sample when the weights are finite
       // with |w| < 1e30 (|pos| <= 5 max|phi w|, |vel| <= 2 |pos| / dt stay far inside f32), the
@@ -698,13 +699,15 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #pragma unroll
         for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.w[d][j]) < 1e30f;
       }
-      if (__ballot(!ok) != 0) nfast = 0;
+      if (__ballot(!ok) != 0) fast_ok = false;
     }
     const int usplit = __builtin_amdgcn_readfirstlane(split);
-    if (__ballot(split != usplit) != 0) nfast = 0;   // the block phases need one split per wave
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) nfast = min(nfast, __shfl_xor(nfast, off, 64));
-    nfast = __builtin_amdgcn_readfirstlane(nfast);
+    if (__ballot(split != usplit) != 0) fast_ok = false;   // the block phases need one split per wave
+    // nfast full 8-blocks, then the remainder before the first sample that needs the generic
+    // path (e.g. 192..198 ahead of step 199) as one partial block of np < 8 samples
+    const int lim2_min = wave_min(lim2);
+    const int nfast = fast_ok ? lim2_min / 8 : 0;
+    const int np = fast_ok ? lim2_min % 8 : 0;
     // Two loops: blocks before the pairwise split push into the level-1 sums a[] only, blocks from
     // the split on into the second-half sums b[] only.  (With a split, L > 128 and the result is
     // first + u: a[] and t are dead after the split, so numpy's level-1 adds there are skipped;
@@ -721,10 +724,23 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
       ps.first = PairwiseSum::comb(ps.a);   // blocks [0, split)
       for (; kb < 8 * nfast; kb += 8) { FGX_BLOCK(2) }
     }
-#undef FGX_BLOCK
-#undef FGX_SAMPLE
     k = 8 * nfast;
     ps.sync_tails();   // fast blocks end on complete 8-blocks: tails = combined accumulators
+    if (np > 0) {
+      if (usplit > 0 && kb >= usplit) {
+        if (kb == usplit) ps.first = PairwiseSum::comb(ps.a);   // the partial block opens the second half
+#define FGX_PART(J) if (J < np) { FGX_SAMPLE(J, 6) }
+        FGX_PART(0) FGX_PART(1) FGX_PART(2) FGX_PART(3) FGX_PART(4) FGX_PART(5) FGX_PART(6)
+      } else {
+#undef FGX_PART
+#define FGX_PART(J) if (J < np) { FGX_SAMPLE(J, 5) }
+        FGX_PART(0) FGX_PART(1) FGX_PART(2) FGX_PART(3) FGX_PART(4) FGX_PART(5) FGX_PART(6)
+      }
+#undef FGX_PART
+      k += np;
+    }
+#undef FGX_BLOCK
+#undef FGX_SAMPLE
   }
   while (!stop && k < Te) {
     stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG || c.sched_state);
