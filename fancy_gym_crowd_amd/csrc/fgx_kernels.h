@@ -768,7 +768,9 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
       if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
     }
   }
-  if (ENV == ENV_SIMPLE && !LOG) v.fk();
+  // the epilogue needs FK of the final q; a last sample at env step >= 199 (always a generic one)
+  // has just computed it for its reward
+  if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();
   const double ret = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
   episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
 }
