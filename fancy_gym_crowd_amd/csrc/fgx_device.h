@@ -13,6 +13,9 @@
 
 namespace fgx {
 
+// two f32 lanes per register pair: v_pk_{fma,mul,add}_f32 operands
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 constexpr int kMaxLinks = 8;
 constexpr int kMaxObs = 3 * kMaxLinks + 5;
 constexpr int kMaxBasis = 16;
@@ -138,6 +141,18 @@ __device__ __forceinline__ float div_rcp(float x, float d, float r) {
   return __builtin_fmaf(e, r, q);
 }
 
+// f64 x + y and x - y issued as v_fma_f64 with a multiplier of 1.0 the compiler cannot see
+// through: bit-identical to the add (x * 1 is exact, one rounding; signed zeros, infinities and
+// NaN-ness as the add), but a lone wave issues v_fma_f64 every ~6 cycles against ~9 for v_add_f64
+// (profiles/r01_valu_rates_operands.jsonl: "v_fma_f64(x,one_vgpr,c)" vs "v_add_f64").
+__device__ __forceinline__ double one64() {
+  double o = 1.0;
+  asm("" : "+s"(o));
+  return o;
+}
+__device__ __forceinline__ double fadd(double x, double y) { return __builtin_fma(x, one64(), y); }
+__device__ __forceinline__ double fsub(double x, double y) { return __builtin_fma(-y, one64(), x); }
+
 __device__ __forceinline__ double div_rcp64(double x, double d, double r) {
   const double q = x * r;
   const double e = __builtin_fma(-q, d, x);
@@ -181,15 +196,15 @@ struct PairwiseSum {
   // caller sets t = comb(a), u = comb(b) after the fast loop (sync_tails).
   template <int J, int PH>
   __device__ __forceinline__ void add_fast(double v) {
-    if (PH & 1) a[J] = a[J] + v;
-    if (PH & 2) b[J] = b[J] + v;
+    if (PH & 1) a[J] = fadd(a[J], v);
+    if (PH & 2) b[J] = fadd(b[J], v);
   }
   // A partial block (fewer than 8 samples, slots J < 7, after sync_tails): the running tail
   // follows each push as numpy's sequential remainder would (push() with j != 7).
   template <int J, int PH>
   __device__ __forceinline__ void add_partial(double v) {
-    if (PH & 1) { a[J] = a[J] + v; t = t + v; }
-    if (PH & 2) { b[J] = b[J] + v; u = u + v; }
+    if (PH & 1) { a[J] = fadd(a[J], v); t = fadd(t, v); }
+    if (PH & 2) { b[J] = fadd(b[J], v); u = fadd(u, v); }
   }
   __device__ __forceinline__ void sync_tails() {
     t = comb(a);

@@ -126,10 +126,18 @@ template <int MP, int NL, int NB, bool DIVREF = false>
 struct Traj {
   static constexpr int NBM = NB ? NB : kGenBasis;           // weight slots per dof
   static constexpr int K = (MP == MP_PRODMP) ? NBM + 3 : NBM;
-  float w[NL][K];          // ProMP: w ; DMP: w' ; ProDMP: [w' (NBM slots), g', c1, c2]
+  // ProMP with >= 2 joints runs the basis contraction on joint pairs (v_pk_fma_f32 / v_pk_mul_f32 /
+  // v_pk_add_f32: two independent IEEE f32 ops per lane and instruction, so each joint's result is
+  // bit-identical to the scalar chain); an odd last joint rides in the low half of a pair whose
+  // high half is zero.
+  static constexpr bool PK = (MP == MP_PROMP) && NL >= 2;
+  static constexpr int NLP = (NL + 1) / 2;
+  float w[PK ? 1 : NL][K]; // ProMP (1 joint): w ; DMP: w' ; ProDMP: [w' (NBM slots), g', c1, c2]
+  f32x2 wp[PK ? NLP : 1][PK ? NBM : 1];   // ProMP (>= 2 joints): weights of joints (2p, 2p + 1)
+  f32x2 cur2[PK ? NLP : 1], vprev2[PK ? NLP : 1];
   float g[NL];             // DMP goal
   float y[NL], z[NL];      // DMP state
-  float cur[NL], vprev[NL];// ProMP look-ahead
+  float cur[NL], vprev[NL];// ProMP look-ahead (1 joint)
   const float* tab;        // row s0 of the basis table: plan sample k reads rows k + 1, k + 2
   int stride, T, nbr;
   float tau32, rtau32;
@@ -137,6 +145,11 @@ struct Traj {
   // row address of an unrolled sample block is then a constant offset from one base
   static constexpr int KS = NB ? ((MP == MP_PRODMP) ? 2 * (NB + 1) + 4 : (NB + 2 + 3) & ~3) : 0;
 
+  // weight j of joint d (any layout)
+  __device__ __forceinline__ float wt(int d, int j) const {
+    if constexpr (PK) return (d & 1) ? wp[d >> 1][j].y : wp[d >> 1][j].x;
+    else return w[d][j];
+  }
   __device__ __forceinline__ int nb() const { return NB ? NB : nbr; }
   __device__ __forceinline__ int str() const { return KS ? KS : stride; }
   __device__ __forceinline__ float div_tau(float x) const { return DIVREF ? x / tau32 : div_rcp(x, tau32, rtau32); }
@@ -147,6 +160,14 @@ struct Traj {
 #pragma unroll
     for (int j = 0; j < NBM; ++j)
       if (NB || j < nbr) acc = __builtin_fmaf(row[j], wd[j], acc);
+    return acc;
+  }
+  // the same chain on a joint pair (the table entry is broadcast to both halves)
+  __device__ __forceinline__ f32x2 chain2(const float* row, const f32x2* wd) const {
+    f32x2 acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < NBM; ++j)
+      if (NB || j < nbr) acc = __builtin_elementwise_fma((f32x2)row[j], wd[j], acc);
     return acc;
   }
   // ProDMP: [basis (nb), goal, y1, y2] . [w', g', c1, c2]; h holds the 3 tail entries at NBM..NBM+2
@@ -171,7 +192,18 @@ struct Traj {
     stride = c.stride; T = T_; tau32 = tau32_; rtau32 = rtau32_; nbr = c.nb;
     tab = tab_ + (size_t)s0_ * str();
     const int n = nb();
-    if (MP == MP_PROMP) {
+    if (MP == MP_PROMP && PK) {
+#pragma unroll
+      for (int p = 0; p < NLP; ++p)
+#pragma unroll
+        for (int j = 0; j < NBM; ++j) {
+          wp[p][j].x = (NB || j < n) ? params[2 * p * n + j] : 0.0f;
+          wp[p][j].y = ((NB || j < n) && 2 * p + 1 < NL) ? params[(2 * p + 1) * n + j] : 0.0f;
+        }
+      const float* r1 = tab + str();
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) { cur2[p] = chain2(r1, wp[p]); vprev2[p] = (f32x2)0.0f; }
+    } else if (MP == MP_PROMP) {
 #pragma unroll
       for (int d = 0; d < NL; ++d)
 #pragma unroll
@@ -222,7 +254,32 @@ struct Traj {
   __device__ __forceinline__ void at(const DevCfg& c, int k, float* pos, float* vel) {
     const float* row = tab + (size_t)(k + 1) * str();
     const int n = nb();
-    if (MP == MP_PROMP) {
+    if (MP == MP_PROMP && PK) {
+      if (MID || k < T - 1) {
+        const float* nrow = row + str();
+        const float dti = row[n], rdt = row[n + 1];
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) {
+          const f32x2 nx = chain2(nrow, wp[p]);
+          const f32x2 x = nx - cur2[p];
+          const f32x2 q = x * rdt;                                    // div_rcp on the pair
+          const f32x2 er = __builtin_elementwise_fma(-q, (f32x2)dti, x);
+          const f32x2 vl = __builtin_elementwise_fma(er, (f32x2)rdt, q);
+          pos[2 * p] = cur2[p].x;
+          vel[2 * p] = vl.x;
+          if (2 * p + 1 < NL) { pos[2 * p + 1] = cur2[p].y; vel[2 * p + 1] = vl.y; }
+          cur2[p] = nx;
+          vprev2[p] = vl;
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) {
+          pos[2 * p] = cur2[p].x;
+          vel[2 * p] = vprev2[p].x;
+          if (2 * p + 1 < NL) { pos[2 * p + 1] = cur2[p].y; vel[2 * p + 1] = vprev2[p].y; }
+        }
+      }
+    } else if (MP == MP_PROMP) {
       if (MID || k < T - 1) {
         const float* nrow = row + str();
         const float dti = row[n], rdt = row[n + 1];
@@ -294,8 +351,8 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * a[d];
-      v.qd[d] = v.qd[d] + inc;
-      v.q[d] = v.q[d] + c.dt * v.qd[d];
+      v.qd[d] = fadd(v.qd[d], inc);
+      v.q[d] = fadd(v.q[d], c.dt * v.qd[d]);
     }
     double ctrl;
     if (F32) {
@@ -306,12 +363,12 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
     } else {
       ctrl = a[0] * a[0];
 #pragma unroll
-      for (int d = 1; d < NL; ++d) ctrl = ctrl + a[d] * a[d];
+      for (int d = 1; d < NL; ++d) ctrl = fadd(ctrl, a[d] * a[d]);
     }
     // MAYFK = false: the caller guarantees st < 199 (fast blocks), no FK code in the loop body
     if (MAYFK && (st >= 199 || fk_always)) v.fk();
     if (MAYFK && st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
-    r.reward = r.rdist - ctrl;
+    r.reward = fsub(r.rdist, ctrl);
     r.rctrl = ctrl;
   } else {   // direct velocity control: HoleReacher, ViaPointReacher
     double acc_cost = 0.0;
@@ -612,7 +669,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       if (CTRL == CTRL_PD) {
-        const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
+        const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
         a[d] = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
         nan_in |= (u != u);
         if (LOG || J < 0) a[d] = (u != u) ? u : a[d];
@@ -697,7 +754,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         ok = ok && __builtin_fabs(v.q[d]) < 1e300 && __builtin_fabs(v.qd[d]) < 1e300 &&
              __builtin_fabs(c.pg[d]) < 1e300 && __builtin_fabs(c.dg[d]) < 1e300;
 #pragma unroll
-        for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.w[d][j]) < 1e30f;
+        for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.wt(d, j)) < 1e30f;
       }
       if (__ballot(!ok) != 0) fast_ok = false;
     }
