@@ -278,16 +278,34 @@ FAST = FULL + [
     # segment lengths 150 / 50 and 170 / 30: the pairwise split (L/2) & ~7 != that of T = 200
     ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(150)}}, 128, 4),
     ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(170)}}, 128, 4),
+    # clip-free blocks (ProMP + PD): waves of unit-scale weights take them, waves with weights x300
+    # (controls beyond +-1000, np.clip active) or mixed lanes take the clipping body
+    ("fancy_ProMP/LongSimpleReacher-v0", None, 320, 3, "clipmix"),
+    ("fancy_ProMP/SimpleReacher-v0", {"controller_kwargs": {"p_gains": 40.0, "d_gains": 3.0}}, 256, 3, "clipmix"),
 ]
 
 
+def param_scale(kind, N):
+    """per-env weight multipliers: wave 0 unit, wave 1 every 9th lane x300, wave 2 all x300,
+    wave 3 x30 (near the clip-free bound), the rest unit"""
+    s = np.ones(N, np.float32)
+    if kind == "clipmix":
+        s[64:128:9] = 300.0
+        s[128:192] = 300.0
+        s[192:256] = 30.0
+    return s
+
+
 @pytest.mark.parametrize("ci", range(len(FAST)))
-def test_bb_fast_path_vs_oracle(ci):
+def test_bb_fast_path_vs_oracle(ci, monkeypatch):
     """info_level 0 runs the unrolled fast loop (fgx_kernels.h k_episode): returns, flags, lengths,
     observations and the full f64 env state after every BB step.  After the first step every
     third env is reset (unseeded, reset_mask) so that lanes of one wave sit at different env
     steps and replanning phases, which the wave-uniform fast-block count must respect."""
-    env_id, over, N, n_bb = FAST[ci]
+    env_id, over, N, n_bb = FAST[ci][:4]
+    scale = param_scale(FAST[ci][4] if len(FAST[ci]) > 4 else None, N)
+    if len(FAST[ci]) > 4:
+        monkeypatch.setenv("FGX_EPISODE_KERNEL", "classic")   # the clip-free blocks live in k_episode
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
     spec = spec_of(env)
     name = NAME[env_id.split("/")[1]]
@@ -297,7 +315,7 @@ def test_bb_fast_path_vs_oracle(ci):
     rng = np.random.default_rng(91)
     n_exact = 0
     for b in range(n_bb):
-        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32) * scale[:, None]
         obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
         r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
         np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
