@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         __builtin_expect(__ballot(nan_in) != 0, 0)) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
+        const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
         if (u != u) a[d] = u;
       }
     }

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(512, FGX_WS_WAVES) void k_episode_ws(DevCfg c, DevS
     bool nan_in = false;
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
-      const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
+      const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
       a[d] = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
       nan_in |= (u != u);
       if (exact_nan) a[d] = (u != u) ? u : a[d];
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(512, FGX_WS_WAVES) void k_episode_ws(DevCfg c, DevS
     if (!exact_nan && __builtin_expect(__ballot(nan_in) != 0, 0)) {
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        const double u = c.pg[d] * ((double)pos[d] - v.q[d]) + c.dg[d] * ((double)vel[d] - v.qd[d]);
+        const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
         if (u != u) a[d] = u;
       }
     }
