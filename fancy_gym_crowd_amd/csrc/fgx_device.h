@@ -199,6 +199,19 @@ struct PairwiseSum {
     if (PH & 1) a[J] = fadd(a[J], v);
     if (PH & 2) b[J] = fadd(b[J], v);
   }
+  // The same with the value given as its negation c (SimpleReacher fast blocks push the reward
+  // 0 - ctrl as acc - ctrl, one instruction less: equal because no accumulator is ever -0 — they
+  // start at +0 and 0 - ctrl is never -0 — so acc + (0 - ctrl) and acc - ctrl round the same sum)
+  template <int J, int PH>
+  __device__ __forceinline__ void sub_fast(double c) {
+    if (PH & 1) a[J] = fsub(a[J], c);
+    if (PH & 2) b[J] = fsub(b[J], c);
+  }
+  template <int J, int PH>
+  __device__ __forceinline__ void sub_partial(double c) {
+    if (PH & 1) { a[J] = fsub(a[J], c); t = fsub(t, c); }
+    if (PH & 2) { b[J] = fsub(b[J], c); u = fsub(u, c); }
+  }
   // A partial block (fewer than 8 samples, slots J < 7, after sync_tails): the running tail
   // follows each push as numpy's sequential remainder would (push() with j != 7).
   template <int J, int PH>

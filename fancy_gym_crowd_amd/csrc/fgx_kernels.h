@@ -693,8 +693,10 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     // ---- env.step
     const StepOut r = substep<ENV, F32, NL, (J < 0)>(c, v, a, a32, fk_always);
     if constexpr (J >= 0) {   // fast blocks: no termination, truncation or replanning inside
-      if constexpr ((PH & 4) != 0) ps.template add_partial<J, (PH & 3)>(r.reward);   // partial block
-      else ps.template add_fast<J, PH>(r.reward);
+      // SimpleReacher below env step 199: reward = 0 - ctrl, pushed as acc - ctrl
+      if constexpr (ENV != ENV_SIMPLE) ps.template add_fast<J, (PH & 3)>(r.reward);   // (not reached)
+      else if constexpr ((PH & 4) != 0) ps.template sub_partial<J, (PH & 3)>(r.rctrl);   // partial block
+      else ps.template sub_fast<J, PH>(r.rctrl);
       return false;
     } else {
       term = (ENV != ENV_SIMPLE) ? r.coll : false;
