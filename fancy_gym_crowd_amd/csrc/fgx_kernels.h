@@ -22,8 +22,11 @@ namespace fgx {
 // Env observation (simple_reacher.py:75-83 / hole_reacher.py:296-306) [+ t/max_steps,
 // utils/wrappers.py:58-59], context-masked when `ctx` (black_box_wrapper.py:90-95), written
 // straight to up to two destinations (no private arrays: nothing spills to scratch).
+// fresh: v was just reset (Env::reset): q = [q0, +0, ..., +0] and fk() has run, so cos / sin of
+// q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
 template <int NL>
-__device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2) {
+__device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
+                                         bool fresh = false) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
@@ -33,8 +36,15 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
   };
   if (rs) {
     double sn[NL], cs[NL];
+    if (fresh) {
+      cs[0] = v.c[0];
+      sn[0] = v.s[0];
 #pragma unroll
-    for (int k = 0; k < NL; ++k) sincos(v.q[k], &sn[k], &cs[k]);
+      for (int k = 1; k < NL; ++k) { cs[k] = 1.0; sn[k] = 0.0; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NL; ++k) sincos(v.q[k], &sn[k], &cs[k]);
+    }
 #pragma unroll
     for (int k = 0; k < NL; ++k) put((float)cs[k]);
 #pragma unroll
@@ -581,7 +591,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
     store_rng(s.rng, N, e, rg);
     plans = 0;
     v.flags = 0;
-    emit_obs(c, v, c.return_context, ob, nullptr);
+    emit_obs(c, v, c.return_context, ob, nullptr, true);
   } else {
     emit_obs(c, v, c.return_context, ob, fo);
   }
