@@ -402,7 +402,23 @@ struct Env {
       cd = 0.0;   // reward_function.reset() (the saved end effector is rewritten before use)
       ex = ey = 0.0;
     }
-    fk();
+    fk_fresh();
+  }
+  // fk() of a freshly reset arm: q = [q0, +0, ..., +0] makes every cumulative angle q0 exactly
+  // (q0 + 0.0 == q0: q0 is never -0), so one sincos serves all links; the running sums are fk()'s
+  __device__ __forceinline__ void fk_fresh() {
+    double sn, cs;
+    sincos(q[0], &sn, &cs);
+    double x = 0.0, y = 0.0;
+    jx[0] = 0.0; jy[0] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      c[k] = cs; s[k] = sn;
+      x = (k == 0) ? cs : x + cs;
+      y = (k == 0) ? sn : y + sn;
+      jx[k + 1] = 0.0 + x;
+      jy[k + 1] = 0.0 + y;
+    }
   }
 
   // ---------------------------------------------------------------- collisions (HoleReacher)

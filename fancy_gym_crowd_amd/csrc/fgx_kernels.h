@@ -24,9 +24,10 @@ namespace fgx {
 // straight to up to two destinations (no private arrays: nothing spills to scratch).
 // fresh: v was just reset (Env::reset): q = [q0, +0, ..., +0] and fk() has run, so cos / sin of
 // q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
+// fk0: FK is current for q (k_episode's epilogue), so cos / sin of q[0] are c[0] / s[0].
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
-                                         bool fresh = false) {
+                                         bool fresh = false, bool fk0 = false) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
@@ -43,7 +44,10 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
       for (int k = 1; k < NL; ++k) { cs[k] = 1.0; sn[k] = 0.0; }
     } else {
 #pragma unroll
-      for (int k = 0; k < NL; ++k) sincos(v.q[k], &sn[k], &cs[k]);
+      for (int k = 0; k < NL; ++k) {
+        if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
+        else sincos(v.q[k], &sn[k], &cs[k]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < NL; ++k) put((float)cs[k]);
@@ -585,7 +589,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   float* ob = o.obs + e * c.out_dim;
   float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
   if (o.autoreset && (term || trunc)) {
-    if (fo) emit_obs(c, v, c.return_context, fo, nullptr);
+    if (fo) emit_obs(c, v, c.return_context, fo, nullptr, false, true);
     Pcg64 rg = load_rng(s.rng, N, e);
     v.reset(c, rg, false, 0);
     store_rng(s.rng, N, e, rg);
@@ -593,7 +597,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
     v.flags = 0;
     emit_obs(c, v, c.return_context, ob, nullptr, true);
   } else {
-    emit_obs(c, v, c.return_context, ob, fo);
+    emit_obs(c, v, c.return_context, ob, fo, false, true);
   }
   store_env(c, s, e, v, c.env != ENV_SIMPLE);
   s.plans[e] = plans;
