@@ -1,8 +1,13 @@
 """Benchmark: inner env-steps/s of fancy_ProMP/LongSimpleReacher-v0 black-box steps on MI355X.
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--envs ENVS_PER_GPU]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--global-envs G | --envs ENVS_PER_GPU]
+
+BASELINE.json's metric is quoted at N = 65536 envs in total over 1/2/4/8 GPUs: the default is
+STRONG scaling (--global-envs 65536, each of the N ranks owns 65536/N envs).  --envs gives every
+rank a fixed number of envs instead (weak scaling).  With N > 1 the strong-scaling line also
+carries a weak-scaling measurement (65536 envs per GPU) as a secondary field.
 For N > 1 launch with torch.distributed.run (one process per GPU); env shards are independent
-(weak scaling: ENVS_PER_GPU envs per rank, seeds = global env index), RCCL only gathers the
+(seeds = global env index, the rank's rows of the global parameter matrix), RCCL only gathers the
 final episode returns.  Prints ONE JSON line on rank 0.
 
 A "step" = one BlackBoxWrapper.step for every env (black_box_wrapper.py:170-253): MP trajectory
@@ -16,75 +21,46 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "inner env-steps/sec, ProMP 5-link Reacher, N=65536 envs at 1/2/4/8 MI355X"
 WORKLOAD = "fancy_ProMP/LongSimpleReacher-v0"
+GLOBAL_ENVS = 65536
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP64_VEC_PEAK_TF = 78.6    # MI355X FP64 vector peak (spec; half the 157.3 TF FP32 vector peak)
+FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector / matrix f32)
+CLOCK_GHZ = 2.4            # MI355X peak engine clock (GRBM_GUI_ACTIVE / kernel time agrees, profiles/)
+# VALU issue: a SIMD issues one wave64 f64 VALU instruction per 4 clocks at best (16 lanes x 4
+# passes); tools/valu_rates.hip measures 4.68 cycles with >= 4 independent waves per SIMD and
+# 6.12 for a lone wave (profiles/r01_valu_rates.jsonl, v_fma_f64 chains)
+ISSUE_ARCH_CYCLES = 4.0
+ISSUE_SIMD_CYCLES = 4.68
+ISSUE_SINGLE_WAVE_CYCLES = 6.12
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
-FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector)
-CLOCK_GHZ = 2.4            # MI355X peak engine clock
-# cycles per VALU instruction a single wave sustains with 8 independent f64 fma chains, and the
-# SIMD with >= 4 waves (profiles/r01_valu_rates.jsonl): k_episode runs one wave per SIMD
-SINGLE_WAVE_CYCLES = 6.12
-SIMD_CYCLES = 4.68
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_k_episode.json")
-PMC_ISSUE = os.path.join(ROOT, "profiles", "r01_pmc_issue_k_episode.json")
-
-
-def pmc_issue(env_id, n_envs):
-    """Issue-side PMC of the metric kernel (committed rocprofv3 passes): VALUBusy and VALU
-    instructions per inner step."""
-    if env_id != WORKLOAD or n_envs != 65536:
-        return None
-    try:
-        with open(PMC_ISSUE) as f:
-            d = json.load(f)
-        c, per = d["counters_per_dispatch"], d["per_wave_sample"]
-        return {"valu_busy_pct": c["VALUBusy"], "valu_lane_util_pct": c["VALUUtilization"],
-                "valu_instr_per_inner_step_per_wave": per["SQ_INSTS_VALU"],
-                "f64_add_mul_fma_per_inner_step_per_wave": per["SQ_INSTS_VALU_ADD_F64"]
-                + per["SQ_INSTS_VALU_MUL_F64"] + per["SQ_INSTS_VALU_FMA_F64"],
-                "source": "profiles/r01_pmc_issue_k_episode.json"}
-    except (OSError, ValueError, KeyError):
-        return None
-
-
-def episode_flops_per_step(env):
-    """Algorithmic flops of one inner env step of k_episode (PD controller, torque env).
-    f32: basis contraction (2 flop per fma) + velocity difference/division;
-    f64: PD (5 per dof), clip (0), Euler (4 per dof), control cost (2 per dof - 1), return (1)."""
-    n, nb = env.dof, 5
-    f32 = n * (2 * nb + 3)
-    f64 = n * 5 + n * 4 + (2 * n - 1) + 1
-    return f32, f64
-
-
-def pmc_traffic(env_id, n_envs):
-    """HBM bytes per k_episode launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 per the
-    gfx950 half-count correction + WRITE_SIZE, KiB -> B), if it was taken on this workload."""
+def pmc_entry(env_id, n_envs, kernel):
+    """Committed rocprofv3 PMC summary of the kernel this run launches (tools/pmc_summary.py):
+    total VALU instructions and HBM bytes per launch; None if that kernel / size was not profiled."""
     try:
         with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-        if d.get("workload") == env_id and int(d.get("envs")) == n_envs:
-            return float(d["traffic_bytes_per_launch"])
+            entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
-        pass
+        return None
+    for e in entries:
+        if e.get("workload") == env_id and int(e.get("envs", -1)) == n_envs and e.get("kernel") == kernel:
+            return e
     return None
 
 
 def episode_bytes_per_env(env):
-    """Algorithmic HBM bytes of one k_episode launch per env (info_level 0, autoreset on)."""
+    """Algorithmic HBM bytes of one episode launch per env (info_level 0, autoreset on)."""
     n, P, out = env.dof, env.n_params, env.out_dim
     hole = 0 if env._eng.cfg.env_kind == 0 else 3 * 8      # SimpleReacher kernels skip hole / aux
     state = 2 * n * 8 + 2 * 8 + hole + 3 * 4 + 5 * 8       # q, qd, goal, [hole], steps/plans/flags, rng
     reads = P * 4 + state
-    writes = state + 2 * out * 4 + 8 + 1 + 1 + 4           # state, obs, final_obs, ret, term, trunc, len
+    writes = state + 8 + 2 * out * 4 + 8 + 1 + 1 + 4       # state + start angle, obs, final_obs, ret, flags, len
     return reads + writes
 
 
@@ -93,11 +69,13 @@ def basis_gemm(env, params, reps=10):
     fgx_trajectory -> k_traj_mfma, v_mfma_f32_32x32x2_f32 with K = 8): time per launch from HIP
     events around a graph replay of `reps` launches, MFMA utilisation against the f32 matrix peak
     and the HBM rate of its [N, T, dof] f32 outputs."""
+    import ctypes
+
+    import torch
     N, T, n = env.num_envs, env.T, env.dof
     pos = torch.empty((N, T, n), dtype=torch.float32, device=params.device)
     vel = torch.empty_like(pos)
     lib, h = env._eng.lib, env._eng.h
-    import ctypes
     args = [ctypes.c_void_p(x.data_ptr()) for x in (params, pos, vel)]
     launch = lambda: lib.fgx_trajectory(h, *args, env._eng.stream())   # noqa: E731
     launch()
@@ -118,25 +96,54 @@ def basis_gemm(env, params, reps=10):
             "peak_tflops": FP32_VEC_PEAK_TF, "mfma_frac": flops / t / 1e12 / FP32_VEC_PEAK_TF,
             "hbm_GBps": out_bytes / t / 1e9, "hbm_frac": out_bytes / t / 1e9 / HBM_PEAK_GBS,
             "note": "K = 8 (5 basis + zero pad): arithmetic intensity 2 flop/B, bound by the output "
-                    "write; the fused k_episode evaluates the same contraction in registers instead"}
+                    "write; the fused episode kernels evaluate the same contraction in registers instead"}
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_share():
+    """CPUs this job may use: the affinity mask, capped by a cgroup CPU quota (cgroup v2
+    cpu.max / v1 cfs_quota) when one is set.  Returns (cpus, affinity, source)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None and quota < aff:
+        return max(1, int(quota)), aff, f"cgroup CPU quota {quota:g} (affinity {aff})"
+    return aff, aff, f"sched_getaffinity ({aff})"
 
 
 def cpu_baseline(seconds=12.0, cores=None):
-    """The oracle port (structure-matched per-env Python loop of the reference) on host cores."""
+    """The oracle port (structure-matched per-env Python loop of the reference) on host cores:
+    one process per usable CPU (cpu_share), each running the loop for `seconds`."""
     import multiprocessing as mp_
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = cores or max(1, min(16, aff))
-    ctx = mp_.get_context("fork")
+    n, aff, source = cpu_share()
+    cores = cores or n
+    ctx = mp_.get_context("fork")   # called before this process touches the GPU (main())
     with ctx.Pool(cores) as pool:
         t0 = time.perf_counter()
         res = pool.map(_cpu_worker, [(i, seconds) for i in range(cores)])
         wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
+    per_core = float(np.mean([r[0] / r[1] for r in res]))
     return dict(value=steps / wall, unit="inner env-steps/s", cores=cores, kind="port",
+                per_core=per_core, affinity_cpus=aff, cores_source=source,
                 sample=f"oracle/port.py per-env loop (f32 ProMP contraction + PD + 200 substeps with the "
                        f"reference's per-step numpy ops incl. its 2 self-collision checks + autoreset), "
                        f"{WORKLOAD}, {cores} processes x ~{seconds:.0f}s, {steps} inner steps; "
-                       f"os.cpu_count()={os.cpu_count()}, affinity={aff}")
+                       f"os.cpu_count()={os.cpu_count()}, usable CPUs from {source}")
 
 
 def _cpu_worker(args):
@@ -170,43 +177,18 @@ def _cpu_worker(args):
     return steps, time.perf_counter() - t0
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--env-id", default=WORKLOAD)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="launch the K steps eagerly instead of replaying them as one HIP graph")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # rehearsal: more ranks than visible GPUs (the 1-GPU dev box) -> all ranks on cuda:0, gloo on
-    # host copies for the collectives; production: one rank per GPU, RCCL ("nccl") over xGMI
-    rehearsal = world > 1 and torch.cuda.device_count() < world
-    gpu = 0 if rehearsal else local
-    coll_dev = "cpu" if rehearsal else torch.device("cuda", gpu)
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(gpu)
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-    dev = torch.device("cuda", gpu)
-    torch.cuda.set_device(dev)
+# ----------------------------------------------------------------------------- GPU run
+def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev):
+    """K timed BB steps of this rank's shard (global envs [rank * n_local, (rank + 1) * n_local)),
+    bracketed by barrier + synchronize on both sides.  Returns wall time (max over ranks), inner
+    steps (sum over ranks), this rank's event time per step, inner steps and the env."""
+    import torch
 
     import fancy_gym_crowd_amd as fgx
     from fancy_gym_crowd_amd import shard
-    N = args.envs
+    N = n_local
     lo, _ = shard.shard_range(N, rank, world)
-    env = fgx.make(args.env_id, num_envs=N, device=dev, seed_offset=lo)
+    env = fgx.make(env_id, num_envs=N, device=dev, seed_offset=lo, info_level=0)
     P = env.n_params
     # MP parameters: default_rng(1234).standard_normal((N_global, P), f32), this rank's rows
     allp = np.random.default_rng(1234).standard_normal((N * world, P), dtype=np.float32)
@@ -220,26 +202,24 @@ def main():
     tl = torch.empty(N, dtype=torch.int32, device=dev)
     acc = torch.zeros(1, dtype=torch.int64, device=dev)   # device counter of inner env steps
 
-    for _ in range(args.warmup):
+    for _ in range(W):
         env.step_into(params, obs, ret, te, tr, tl, fobs)
     torch.cuda.synchronize()
-    acc.zero_()
-
-    K = args.steps
     graph = None
-    if args.graph:
+    if use_graph:
         # the K BB-step launches captured once in a HIP graph (the same kernels on the same state;
         # removes the per-launch host round trip between dependent steps)
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                for k in range(K):
+                for _ in range(K):
                     env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
             torch.cuda.synchronize()
         except Exception as e:   # capture unsupported: time the eager launches instead
             print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
             graph = None
     acc.zero_()
+    # HIP events on the stream the kernels are launched on (the current stream of step_into)
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     if dist is not None:
@@ -262,7 +242,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     inner_local = int(acc.item())
-    if graph is not None:   # HIP events around the replay on the launch stream: mean per BB step
+    if graph is not None:
         kern_ms = ev0[0].elapsed_time(ev1[0]) / K
     else:
         kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
@@ -272,61 +252,135 @@ def main():
         assert all_ret.numel() == N * world
     else:
         inner = inner_local
+    return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
+                launch="hip graph of the K steps" if graph is not None else "eager")
+
+
+def roofline(env_id, env, N, kern_ms, inner_local, K, simds):
+    """Roofline of the episode kernel.  Its state stays in registers for all T substeps, so the
+    binding resource is VALU instruction issue: achieved = VALU wave-instructions per SIMD per
+    clock over the kernel time (instruction count from the committed rocprofv3 PMC pass of this
+    kernel and size), peak = the measured multi-wave issue floor.  HBM is reported beside it."""
+    kernel = env.episode_kernel()
+    bpe = episode_bytes_per_env(env)
+    hbm_gbs = bpe * N / (kern_ms * 1e-3) / 1e9
+    pmc = pmc_entry(env_id, N, kernel)
+    hbm = {"achieved_GBps": hbm_gbs, "peak_GBps": HBM_PEAK_GBS, "frac": hbm_gbs / HBM_PEAK_GBS,
+           "algorithmic_bytes_per_env": bpe, "algorithmic_bytes_per_launch": bpe * N,
+           "bytes_per_inner_step": bpe * N / max(1, inner_local / K)}
+    out = {"kernel": kernel, "kernel_ms": kern_ms, "hbm": hbm}
+    if pmc is not None:
+        cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
+        achieved = pmc["valu_instr_per_launch"] / simds / cyc
+        peak = 1.0 / ISSUE_SIMD_CYCLES
+        traffic = pmc.get("traffic_bytes_per_launch")
+        hbm["traffic_over_algorithmic"] = traffic / (bpe * N) if traffic else None
+        out.update({"bound": "valu_issue", "achieved": achieved, "peak": peak,
+                    "unit": "VALU wave-instr/cycle/SIMD", "frac": achieved / peak, "traffic": traffic,
+                    "peak_note": f"peak = 1/{ISSUE_SIMD_CYCLES} (measured >=4-wave f64 issue floor; the "
+                                 f"architectural 1/{ISSUE_ARCH_CYCLES:g} gives frac "
+                                 f"{achieved * ISSUE_ARCH_CYCLES:.3f}; a lone wave sustains 1/"
+                                 f"{ISSUE_SINGLE_WAVE_CYCLES})",
+                    "pmc": {k: pmc.get(k) for k in ("valu_instr_per_launch", "valu_instr_per_inner_step_per_env",
+                                                    "valu_busy_pct", "waves", "kernel_ns_median_under_pmc",
+                                                    "build_id", "source")}})
+    else:   # no PMC pass of this kernel / size committed: the HBM roofline alone
+        out.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_gbs / HBM_PEAK_GBS, "traffic": None,
+                    "note": "no committed PMC pass for this kernel and size (profiles/pmc_summary.json)"})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--global-envs", type=int, default=GLOBAL_ENVS,
+                    help="total envs over all ranks (strong scaling, the metric's definition)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (weak scaling instead)")
+    ap.add_argument("--env-id", default=WORKLOAD)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="launch the K steps eagerly instead of replaying them as one HIP graph")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU baseline runs first, before this process touches the GPU (its workers are forked)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    import torch
+    dist = None
+    # rehearsal: more ranks than visible GPUs (the 1-GPU dev box) -> all ranks on cuda:0, gloo on
+    # host copies for the collectives; production: one rank per GPU, RCCL ("nccl") over xGMI
+    rehearsal = world > 1 and torch.cuda.device_count() < world
+    gpu = 0 if rehearsal else local
+    coll_dev = "cpu" if rehearsal else torch.device("cuda", gpu)
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(gpu)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(dev)
+
+    strong = args.envs is None
+    if strong:
+        if args.global_envs % world:
+            raise SystemExit(f"--global-envs {args.global_envs} does not split over {world} ranks")
+        n_local = args.global_envs // world
+    else:
+        n_local = args.envs
+    K, W = args.steps, args.warmup
+    r = run_shard(args.env_id, n_local, rank, world, K, W, args.graph, dev, dist, coll_dev)
+    weak = None
+    if strong and world > 1 and not args.no_weak:   # secondary: 65536 envs per GPU
+        w = run_shard(args.env_id, GLOBAL_ENVS, rank, world, K, W, args.graph, dev, dist, coll_dev)
+        weak = {"envs_per_gpu": GLOBAL_ENVS, "global_envs": GLOBAL_ENVS * world, "value": w["inner"] / w["elapsed"],
+                "ms_per_step": w["elapsed"] / K * 1e3, "kernel": w["env"].episode_kernel(),
+                "kernel_ms": w["kern_ms"]}
+        del w
 
     if rank == 0:
-        value = inner / elapsed
-        f32f, f64f = episode_flops_per_step(env)
-        steps_per_s_kernel = (inner_local / K) / (kern_ms * 1e-3)
-        valu = {"f32_tflops": f32f * steps_per_s_kernel / 1e12, "f64_tflops": f64f * steps_per_s_kernel / 1e12,
-                "peak_f32_tflops": FP32_VEC_PEAK_TF, "peak_f64_tflops": FP64_VEC_PEAK_TF,
-                "frac": f32f * steps_per_s_kernel / 1e12 / FP32_VEC_PEAK_TF
-                + f64f * steps_per_s_kernel / 1e12 / FP64_VEC_PEAK_TF,
-                "pmc": pmc_issue(args.env_id, N)}
-        if valu["pmc"] is not None:   # issue rate: VALU instructions per SIMD over the kernel time
-            instr = valu["pmc"]["valu_instr_per_inner_step_per_wave"] * (inner_local / K) / 64.0
-            simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-            cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9 / (instr / simds)
-            valu["issue"] = {"cycles_per_valu_instr_per_simd": cyc,
-                             "single_wave_floor_cycles": SINGLE_WAVE_CYCLES, "simd_floor_cycles": SIMD_CYCLES,
-                             "frac_of_single_wave_issue": SINGLE_WAVE_CYCLES / cyc,
-                             "frac_of_simd_issue": SIMD_CYCLES / cyc,
-                             "note": "one wave (64 envs) per SIMD at 65536 envs: the single-wave issue rate "
-                                     "is the ceiling (DESIGN.md 4.3)"}
-        bpe = episode_bytes_per_env(env)
-        achieved = bpe * N / (kern_ms * 1e-3) / 1e9
+        env = r["env"]
+        simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         line = {
             "metric": METRIC,
-            "value": value,
+            "value": r["inner"] / r["elapsed"],
             "unit": "inner env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / K * 1e3,
+            "warmup": W,
+            "ms_per_step": r["elapsed"] / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: reset(seed=0) -> env i seeded with its global index; MP params "
                     "default_rng(1234).standard_normal((N_global, 25), f32)",
-            "config": {"workload": args.env_id, "envs_per_gpu": N, "global_envs": N * world, "T": env.T,
-                       "launch": "hip graph of the K steps" if graph is not None else "eager",
+            "config": {"workload": args.env_id, "global_envs": n_local * world, "envs_per_gpu": n_local,
+                       "T": env.T, "launch": r["launch"],
                        "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"
                        + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args.env_id, N),
-                         "kernel": env.episode_kernel(), "kernel_ms": kern_ms, "bytes_per_env": bpe,
-                         "bytes_per_inner_step": bpe * N / (inner_local / K),
-                         "note": "state lives in registers for all T substeps: the kernel is VALU-issue "
-                                 "bound (see valu); per-substep HBM design would need 242 B/step",
-                         "valu": valu},
+            "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds),
         }
+        if weak is not None:
+            line["weak_scaling"] = weak
         if world == 1 and env.T % 4 == 0:
             try:
-                line["basis_gemm"] = basis_gemm(env, params)
+                line["basis_gemm"] = basis_gemm(env, r["params"])
             except Exception as e:   # report, never fail the bench line on the side measurement
                 line["basis_gemm"] = {"error": str(e)}
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -2,9 +2,15 @@
 
 Translation units are compiled in parallel (the episode kernels of each env kind live in their
 own TU) and linked into one shared library.
+
+Build provenance: the library carries ``fgx_build_id()``, a hash of the sources it was compiled
+from (csrc/*.h, csrc/*.hip, include/fgx.h and the compiler flags).  ``build()`` recompiles
+whenever that hash differs from the one recorded for the existing library, and ``_lib.load()``
+refuses a library whose id does not match the sources next to it.
 """
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -13,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INC = os.path.join(HERE, "..", "include")
 LIB = os.path.join(HERE, "libfgx.so")
+STAMP = LIB + ".buildid"
 OBJDIR = os.path.join(HERE, "csrc", "build")
 SOURCES = ["fgx_ep_simple_gen.hip", "fgx_ep_hole_gen.hip", "fgx_ep_via_gen.hip", "fgx_ep_simple.hip",
            "fgx_ep_hole.hip", "fgx_ep_via.hip", "fgx_api.hip"]
@@ -22,27 +29,37 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-Wno-unused-result"]
 
 
-def _deps():
-    return (glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip")) +
-            [os.path.join(INC, "fgx.h"), os.path.abspath(__file__)])
+def source_files():
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip"))) + \
+        [os.path.join(INC, "fgx.h")]
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+def source_hash():
+    """16 hex digits of sha256 over the source files (name + bytes) and the compiler flags."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for f in source_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def built_id():
+    """Build id recorded for the existing library (None if missing)."""
+    if not (os.path.exists(LIB) and os.path.exists(STAMP)):
+        return None
+    with open(STAMP) as f:
+        return f.read().strip()
 
 
 def _hipcc():
     return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def _compile(src, verbose):
+def _compile(src, bid, verbose):
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
-    if not _stale(obj, _deps()):
-        return obj
-    cmd = [_hipcc(), *FLAGS, "-I", INC, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
+    cmd = [_hipcc(), *FLAGS, f'-DFGX_BUILD_ID="{bid}"', "-I", INC, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -51,19 +68,19 @@ def _compile(src, verbose):
 
 
 def build(force=False, verbose=True):
-    if not force and not _stale(LIB, _deps()):
+    bid = source_hash()
+    if not force and built_id() == bid:
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
-    if force:
-        for f in glob.glob(os.path.join(OBJDIR, "*.o")):
-            os.remove(f)
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, bid, verbose), SOURCES))
     cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    with open(STAMP, "w") as f:
+        f.write(bid + "\n")
     return LIB
 
 

@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 4
+FGX_ABI_VERSION = 5
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
 SCHED_EVERY, SCHED_AT, SCHED_NORM_PERIOD = 0, 1, 2
@@ -58,11 +58,12 @@ class FgxInfo(ctypes.Structure):
 EXPORTS = {
     "fgx_last_error": (ctypes.c_char_p, []),
     "fgx_abi_version": (ctypes.c_int, []),
+    "fgx_build_id": (ctypes.c_char_p, []),
     "fgx_create": (ctypes.c_int, [ctypes.POINTER(FgxConfig), ctypes.c_int64, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_void_p)]),
     "fgx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fgx_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FgxDims)]),
-    "fgx_reset": (ctypes.c_int, [ctypes.c_void_p] * 5),
+    "fgx_reset": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int32] + [ctypes.c_void_p] * 2),
     "fgx_step": (ctypes.c_int, [ctypes.c_void_p] * 8 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
                                                          ctypes.c_void_p]),
     "fgx_step_traj": (ctypes.c_int, [ctypes.c_void_p] * 9 + [ctypes.POINTER(FgxInfo), ctypes.c_int32,
@@ -85,7 +86,8 @@ class FgxError(RuntimeError):
 
 def load(path=None):
     """Load libfgx.so and declare every exported symbol (no GPU needed).  FGX_LIB names another
-    build of the same ABI (kernel experiments); the default is the in-tree library."""
+    build of the same ABI (kernel experiments; its build id is not checked); the default is the
+    in-tree library, whose build id must match the in-tree sources (_build.source_hash)."""
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -100,6 +102,12 @@ def load(path=None):
         fn.argtypes = args
     if lib.fgx_abi_version() != FGX_ABI_VERSION:
         raise FgxError("libfgx ABI version mismatch")
+    if path == LIB_PATH:   # build provenance: the in-tree library must match the in-tree sources
+        from . import _build
+        want, got = _build.source_hash(), lib.fgx_build_id().decode()
+        if got != want:
+            raise FgxError(f"libfgx.so was built from other sources (build id {got}, sources {want}); "
+                           "run __graft_entry__.build()")
     _LIB = lib
     return lib
 

@@ -74,12 +74,13 @@ static int launch_episode(const Handle& h, int mp, const float* params, const fl
                                                                      g_err);
 }
 
-static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, float* obs, hipStream_t stream) {
+static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* mask, int rs_mode, float* obs,
+                        hipStream_t stream) {
   const int threads = 256;
   const int blocks = (int)((h.dc.N + threads - 1) / threads);
-#define X(NL)                                                                                             \
-  if (h.dc.nl == NL) {                                                                                    \
-    hipLaunchKernelGGL((k_reset<NL>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, seeds, mask, obs); \
+#define X(NL)                                                                                                    \
+  if (h.dc.nl == NL) {                                                                                           \
+    hipLaunchKernelGGL((k_reset<NL>), dim3(blocks), dim3(threads), 0, stream, h.dc, h.st, seeds, mask, rs_mode, obs); \
     HIP_TRY(hipGetLastError());                                                                           \
     return FGX_OK;                                                                                        \
   }
@@ -238,11 +239,12 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.rand_x = std::isnan(c.hole_x);
   d.rand_depth = std::isnan(c.hole_depth);
   d.rew_fct = c.rew_fct;
-  if (c.env_kind == FGX_ENV_VIA && (std::isnan(c.via_x) != std::isnan(c.via_y) ||
-                                    std::isnan(c.target_x) != std::isnan(c.target_y)))
-    return fail(FGX_E_INVALID, "via_target / target must be given as (x, y) or left unset");
+  if (c.env_kind == FGX_ENV_VIA && std::isnan(c.via_x) != std::isnan(c.via_y))
+    return fail(FGX_E_INVALID, "via_target must be given as (x, y) or left unset");
+  if (c.env_kind != FGX_ENV_HOLE && std::isnan(c.target_x) != std::isnan(c.target_y))
+    return fail(FGX_E_INVALID, "target must be given as (x, y) or left unset");
   d.rand_via = std::isnan(c.via_x);
-  d.rand_target = std::isnan(c.target_x);
+  d.rand_target = c.env_kind == FGX_ENV_HOLE || std::isnan(c.target_x);   // SimpleReacher / ViaPointReacher target
   d.via_x0 = c.via_x; d.via_y0 = c.via_y;
   d.tgt_x0 = c.target_x; d.tgt_y0 = c.target_y;
   d.dt = c.dt;
@@ -285,6 +287,11 @@ const char* fgx_last_error(void) { return g_err.c_str(); }
 
 int fgx_abi_version(void) { return FGX_ABI_VERSION; }
 
+#ifndef FGX_BUILD_ID
+#define FGX_BUILD_ID "unknown"
+#endif
+const char* fgx_build_id(void) { return FGX_BUILD_ID; }
+
 int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle) {
   if (!cfg || !handle) return fail(FGX_E_INVALID, "null argument");
   *handle = nullptr;
@@ -309,6 +316,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_rng = off; off = align_up(off + sizeof(uint64_t) * 5 * N);
   const size_t o_cond = off; off = align_up(off + sizeof(float) * 2 * nl * N);
   const size_t o_seed = off; off = align_up(off + sizeof(uint64_t) * N);
+  const size_t o_start = off; off = align_up(off + sizeof(double) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
   // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128)
   const bool need_rew = (cfg->env_kind != FGX_ENV_SIMPLE || h->dc.sched_state) && cfg->mp_kind != FGX_MP_NONE &&
@@ -331,6 +339,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.rew = need_rew ? (double*)(b + o_rew) : nullptr;
   h->st.plan_len = nullptr;
   h->st.tables = h->tables;
+  h->st.start = (double*)(b + o_start);
   (void)hipMemset(h->state_block, 0, off);
   if (h->learned()) {
     const DevCfg& d0 = h->dc;
@@ -361,16 +370,23 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   }
   e = hipGetLastError();
   if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("table kernel: ") + hipGetErrorString(e)); }
-  // a deterministic first reset (seed = env index) so that the state is always valid
+  // _start_pos[0] of a fresh env (simple_reacher.py:29 zeros; base_reacher.py:34 pi/2), then a
+  // deterministic first reset (seed = env index) so that the state is always valid
   uint64_t* seeds = (uint64_t*)(b + o_seed);
   {
     uint64_t* hs = new uint64_t[N];
-    for (int64_t i = 0; i < N; ++i) hs[i] = (uint64_t)i;
+    double* sp = new double[N];
+    for (int64_t i = 0; i < N; ++i) {
+      hs[i] = (uint64_t)i;
+      sp[i] = cfg->env_kind == FGX_ENV_SIMPLE ? 0.0 : M_PI / 2;
+    }
     e = hipMemcpy(seeds, hs, sizeof(uint64_t) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->st.start, sp, sizeof(double) * N, hipMemcpyHostToDevice);
     delete[] hs;
+    delete[] sp;
     if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, "hipMemcpy seeds"); }
   }
-  rc = launch_reset(*h, seeds, nullptr, nullptr, 0);
+  rc = launch_reset(*h, seeds, nullptr, -1, nullptr, 0);
   if (rc) { fgx_destroy(h); return rc; }
   e = hipDeviceSynchronize();
   if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("create sync: ") + hipGetErrorString(e)); }
@@ -405,10 +421,12 @@ int fgx_get_dims(void* handle, fgx_dims* out) {
   return FGX_OK;
 }
 
-int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, float* obs_out, void* stream) {
+int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, int32_t random_start, float* obs_out,
+              void* stream) {
   Handle* h = (Handle*)handle;
   if (!h) return fail(FGX_E_INVALID, "null handle");
-  return launch_reset(*h, seeds, mask, obs_out, (hipStream_t)stream);
+  if (random_start < -1 || random_start > 1) return fail(FGX_E_INVALID, "random_start must be -1, 0 or 1");
+  return launch_reset(*h, seeds, mask, random_start, obs_out, (hipStream_t)stream);
 }
 
 static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, int32_t* tlen, float* fobs,

@@ -75,6 +75,7 @@ struct DevState {
                    //     bit2: vel_acc reward function's sticky collision flag
   uint64_t* rng;   // [5][N]  state hi, state lo, inc hi, inc lo, (has_u32 << 32 | u32)
   float* cond;     // [2][nl][N] condition_on_desired pos / vel
+  double* start;   // [N] _start_pos[0] (Env::sp)
   double* rew;     // [T][N] step rewards of the current BB step (direct envs with T > 128 only):
                    //        the exact numpy pairwise return for lengths 128 < L <= T
   const int32_t* plan_len;   // [N] per-env plan length (learned tau / sub-trajectories) or null
@@ -285,6 +286,8 @@ struct Env {
   double gx, gy;
   double hx, hw, hd;     // HoleReacher hole | ViaPointReacher via point (hx, hw)
   double ex, ey, cd;     // HoleReacher reward-function state (aux)
+  double sp;             // _start_pos[0] (base_reacher.py:81-86): the first joint a non-random reset
+                         // restores; a random reset draws it and keeps it
   int steps;
   uint32_t flags;
   // forward kinematics (base_reacher.py:95-103): joints[k+1] = cumsum of (cos, sin)(cumsum q)
@@ -308,12 +311,15 @@ struct Env {
   }
 
   // reset draws (simple_reacher.py:46-54,85-96; hole_reacher.py:242-294; base_reacher.py:73-93)
-  __device__ __forceinline__ void first_joint(const DevCfg& cf, Pcg64& r) {
-    if (cf.random_start) {
+  // rs: random_start of this reset (the constructor's, or reset(options={'random_start': ...}),
+  // base_reacher.py:77-80)
+  __device__ __forceinline__ void first_joint(Pcg64& r, bool rs) {
+    if (rs) {
       const double lo = M_PI / 4, hi = 3 * M_PI / 4;
       q[0] = rng_uniform(r, lo, hi);
+      sp = q[0];
     } else {
-      q[0] = (cf.env == ENV_SIMPLE) ? 0.0 : M_PI / 2;
+      q[0] = sp;
     }
 #pragma unroll
     for (int k = 1; k < NL; ++k) q[k] = 0.0;
@@ -323,7 +329,11 @@ struct Env {
     flags = 0;
   }
 
-  __device__ __forceinline__ void goal_sample(Pcg64& r) {
+  __device__ __forceinline__ void goal_sample(const DevCfg& cf, Pcg64& r) {
+    if (!cf.rand_target) {   // SimpleReacherEnv(target=...) (simple_reacher.py:93-94): no draws
+      gx = cf.tgt_x0; gy = cf.tgt_y0;
+      return;
+    }
     const double total = (double)NL;    // np.sum(link_lengths), unit links
     double g0 = total, g1 = total;
     while (norm2(g0, g1) >= total) {
@@ -379,26 +389,29 @@ struct Env {
   // SimpleReacher and ViaPointReacher sample their goal(s), reset, sample again, reset again
   // (simple_reacher.py:46-54, viapoint_reacher.py:46-54).
   __device__ __forceinline__ void reset(const DevCfg& cf, Pcg64& r, bool seeded, uint64_t seed) {
+    reset(cf, r, seeded, seed, cf.random_start != 0);
+  }
+  __device__ __forceinline__ void reset(const DevCfg& cf, Pcg64& r, bool seeded, uint64_t seed, bool rs) {
     if (cf.env != ENV_HOLE) {
       const bool via = (cf.env == ENV_VIA);
       if (!via) { hx = 0.0; hw = 0.0; hd = 0.0; }   // unused by SimpleReacher: keep the state defined
       if (seeded) {
         pcg_seed(r, seed);
-        first_joint(cf, r);
-        if (via) via_sample(cf, r); else goal_sample(r);
+        first_joint(r, rs);
+        if (via) via_sample(cf, r); else goal_sample(cf, r);
         pcg_seed(r, seed);
-        first_joint(cf, r);
+        first_joint(r, rs);
       } else {
-        if (via) via_sample(cf, r); else goal_sample(r);
-        first_joint(cf, r);
-        if (via) via_sample(cf, r); else goal_sample(r);
-        first_joint(cf, r);
+        if (via) via_sample(cf, r); else goal_sample(cf, r);
+        first_joint(r, rs);
+        if (via) via_sample(cf, r); else goal_sample(cf, r);
+        first_joint(r, rs);
       }
       ex = ey = cd = 0.0;
     } else {
       if (seeded) pcg_seed(r, seed);
       hole_sample(cf, r);
-      first_joint(cf, r);
+      first_joint(r, rs);
       cd = 0.0;   // reward_function.reset() (the saved end effector is rewritten before use)
       ex = ey = 0.0;
     }

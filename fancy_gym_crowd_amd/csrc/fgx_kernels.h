@@ -112,16 +112,41 @@ __device__ __forceinline__ void store_env(const DevCfg& c, const DevState& s, in
 }
 
 // ============================================================================ reset
+// An unseeded reset of env e in registers (VectorEnv auto-reset: env.reset() without options, so
+// the constructor's random_start): the PCG64 stream continues; the start angle is restored
+// (random_start False) or drawn and kept (True).  Callers store the env state afterwards.
+template <int NL>
+__device__ __forceinline__ void autoreset_env(const DevCfg& c, const DevState& s, int64_t e, Env<NL>& v) {
+  Pcg64 rg = load_rng(s.rng, c.N, e);
+  if (!c.random_start) v.sp = s.start[e];
+  v.reset(c, rg, false, 0);
+  store_rng(s.rng, c.N, e, rg);
+  if (c.random_start) s.start[e] = v.sp;
+}
+
+// rs_mode: -1 = the constructor's random_start, 0 / 1 = reset(options={'random_start': ...})
+// (base_reacher.py:77-80).  Envs outside the mask are not reset; their current observation is
+// written to their obs row.
 template <int NL>
 __global__ __launch_bounds__(256) void k_reset(DevCfg c, DevState s, const uint64_t* seeds, const uint8_t* mask,
-                                               float* obs) {
+                                               int rs_mode, float* obs) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= c.N) return;
-  if (mask && !mask[e]) return;
   Env<NL> v;
+  if (mask && !mask[e]) {
+    if (obs) {
+      load_env(c, s, e, v);
+      v.fk();
+      emit_obs(c, v, c.return_context, obs + e * c.out_dim, nullptr);
+    }
+    return;
+  }
+  const bool rs = rs_mode < 0 ? c.random_start != 0 : rs_mode != 0;
   Pcg64 r = load_rng(s.rng, c.N, e);
-  v.reset(c, r, seeds != nullptr, seeds ? seeds[e] : 0);
+  v.sp = s.start[e];
+  v.reset(c, r, seeds != nullptr, seeds ? seeds[e] : 0, rs);
   store_rng(s.rng, c.N, e, r);
+  if (rs) s.start[e] = v.sp;
   store_env(c, s, e, v);
   s.plans[e] = 0;
   s.flags[e] = 0;
@@ -590,9 +615,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
   if (o.autoreset && (term || trunc)) {
     if (fo) emit_obs(c, v, c.return_context, fo, nullptr, false, true);
-    Pcg64 rg = load_rng(s.rng, N, e);
-    v.reset(c, rg, false, 0);
-    store_rng(s.rng, N, e, rg);
+    autoreset_env(c, s, e, v);
     plans = 0;
     v.flags = 0;
     emit_obs(c, v, c.return_context, ob, nullptr, true);
@@ -760,15 +783,18 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     const int lim2 = min(Te - 1, max(0, lim));   // fast samples k < lim2 (sample Te - 1 ends the plan)
     bool fast_ok = __ballot(1) == ~0ull;   // partial wave (N % 64 != 0): generic path only
     if (MP == MP_PROMP && CTRL == CTRL_PD) {
-      // NaN-free waves: the PD control u is finite for every sample when the weights are finite
-      // with |w| < 1e30 (|pos| <= 5 max|phi w|, |vel| <= 2 |pos| / dt stay far inside f32), the
-      // gains are finite and |q|, |qd| < 1e300 (200 Euler steps with |a| <= 1000 cannot overflow);
-      // the fast blocks then skip np.clip's NaN fix-up, other waves take the exact generic path
-      bool ok = true;
+      // NaN-free waves: the PD control u = p (pos - q) + d (vel - qd) is finite for every sample
+      // of the plan when, for every lane, |w| < 1e30 and |q|, |qd|, |p|, |d| < 1e150:
+      //   |pos| <= sum_j phi_j |w_j| < 1e30 (normalised basis), |vel| <= 2 |pos| / dt < 2e32
+      //   (finite in f32); the clipped |a| <= act_hi = 1000 bounds 200 Euler steps to
+      //   |qd| < 1e150 + 2e3, |q| < 3.1e150, so |p (pos - q)|, |d (vel - qd)| < 4e300 and their
+      //   sum < 8e300 < DBL_MAX: no inf - inf, no 0 * inf, no overflow.
+      // The fast blocks then skip np.clip's NaN fix-up; other waves take the exact generic path.
+      bool ok = __builtin_fabs(c.act_lo) <= 1e3 && __builtin_fabs(c.act_hi) <= 1e3 && c.dt <= 1.0;
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        ok = ok && __builtin_fabs(v.q[d]) < 1e300 && __builtin_fabs(v.qd[d]) < 1e300 &&
-             __builtin_fabs(c.pg[d]) < 1e300 && __builtin_fabs(c.dg[d]) < 1e300;
+        ok = ok && __builtin_fabs(v.q[d]) < 1e150 && __builtin_fabs(v.qd[d]) < 1e150 &&
+             __builtin_fabs(c.pg[d]) < 1e150 && __builtin_fabs(c.dg[d]) < 1e150;
 #pragma unroll
         for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.wt(d, j)) < 1e30f;
       }
@@ -871,9 +897,7 @@ __global__ __launch_bounds__(256) void k_step_raw(DevCfg c, DevState s, const fl
   float* fo = final_obs ? final_obs + e * c.obs_dim : nullptr;
   if (autoreset && (te || tr)) {
     if (fo) emit_obs(c, v, false, fo, nullptr);
-    Pcg64 rg = load_rng(s.rng, N, e);
-    v.reset(c, rg, false, 0);
-    store_rng(s.rng, N, e, rg);
+    autoreset_env(c, s, e, v);
     v.flags = 0;
     emit_obs(c, v, false, ob, nullptr);
   } else {

@@ -347,11 +347,16 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
                 setattr(c, fy, float(v[1]))
     else:
         bound = 1000.0                                          # base_reacher_torque.py:16-18
-        if kw.get('target') is not None:
-            raise NotImplementedError("SimpleReacher with a fixed target")
+        if kw.get('target') is not None:                        # simple_reacher.py:19,93-94
+            v = np.asarray(kw['target'], dtype=np.float64).reshape(-1)
+            if v.shape != (2,):
+                raise ValueError("target must be an (x, y) pair")
+            c.target_x, c.target_y = float(v[0]), float(v[1])
     c.act_low, c.act_high = -bound, bound
+    # verbose: BlackBoxWrapper.step(action, verbose=2) — the reference's step always assembles the
+    # verbose-2 info (black_box_wrapper.py:170,185,244-249) whatever black_box_kwargs['verbose'] is
     meta = dict(env_id=env_id, base_id=base_id, mp_type=mp_type, kind=spec.kind, n_links=n,
-                reward_aggregation='sum', verbose=1)
+                reward_aggregation='sum', verbose=2)
     if mp_type is None:                                          # step-based env
         c.mp_kind = _lib.MP_NONE
         c.T = 1
@@ -471,13 +476,16 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c.delay_bound_lo, c.delay_bound_hi = float(db[0]), float(db[1])
     if learn_delay and tg_type == 'prodmp':
         raise NotImplementedError("ProDMP with learn_delay")
+    # reward_aggregation (black_box_wrapper.py:252): np.sum / np.mean run in the episode kernel
+    # (numpy's pairwise sum); any other callable is applied to each env's rewards[:t+1]
     agg = bb.get('reward_aggregation', np.sum)
     if agg is np.sum:
         meta['reward_aggregation'] = 'sum'
     elif agg is np.mean:
         meta['reward_aggregation'] = 'mean'
+    elif callable(agg):
+        meta['reward_aggregation'] = agg
     else:
-        raise NotImplementedError("reward_aggregation other than np.sum / np.mean")
-    meta['verbose'] = int(bb.get('verbose', 1))
+        raise ValueError("reward_aggregation must be callable")
     meta['n_params'] = n * c.n_basis + (0 if tg_type == 'promp' else n) + int(learn_tau) + int(learn_delay)
     return c, meta

@@ -6,8 +6,17 @@ The Python surface mirrors what a user of the reference gets from
   step(actions)        -> (obs, reward [N] f64, terminated [N] bool, truncated [N] bool, info)
                                                                   (black_box_wrapper.py:170-253)
 with gymnasium 0.29 vector semantics [EXT-M]: reset(seed=s) seeds env i with s + i; finished
-envs are auto-reset inside step() and their last observation is in
-info['final_observation'] with the boolean mask info['_final_observation'].
+envs are auto-reset inside step(), their last observation is in info['final_observation'] and
+the info of their last step in info['final_info'] (boolean masks '_final_observation' /
+'_final_info').
+
+info levels (BlackBoxWrapper.step assembles its info per verbosity, black_box_wrapper.py:185-249;
+the reference's step(action, verbose=2) default means a gym.make user always gets level 2):
+  0  trajectory_length only (the fast path; bench.py)
+  1  + the env's per-step info lists: reward_dist / reward_ctrl (SimpleReacher,
+     simple_reacher.py:56-70) or is_collided / is_success / end_effector (Hole / ViaPoint)
+  2  + positions, velocities, step_actions, step_observations, step_rewards   (default)
+Per-step arrays are [N, T, ...], NaN (0 for flags) after each env's trajectory_length.
 
 All compute runs in libfgx.so (HIP) on the tensors' device; there is no CPU fallback.
 """
@@ -79,6 +88,51 @@ class _Engine:
             pass
 
 
+class FinalInfo:
+    """info['final_info'] of gymnasium 0.29's SyncVectorEnv [EXT-M]: entry i is the info dict env i
+    produced on the step that ended its episode (the reference's BlackBoxWrapper.step infos:
+    trajectory_length, the per-step lists cut at trajectory_length, the full desired plan), None
+    for envs that did not finish.  Entries are built on access (numpy, host), so step() itself
+    stays free of host synchronisation."""
+
+    _FULL = ("positions", "velocities")   # black_box_wrapper.py:245-246: the whole plan
+
+    def __init__(self, done, per_env):
+        self._done_t = done
+        self._done = None
+        self._per_env = per_env
+        self._host = None
+
+    def _sync(self):
+        if self._done is None:
+            self._done = self._done_t.detach().cpu().numpy().astype(bool)
+            self._host = {k: v.detach().cpu().numpy() for k, v in self._per_env.items()}
+        return self._done
+
+    def __len__(self):
+        return int(self._done_t.shape[0])
+
+    def __getitem__(self, i):
+        done = self._sync()
+        if not done[i]:
+            return None
+        if "trajectory_length" not in self._host:   # step-based envs: no per-step info is kept
+            return {}
+        L = int(self._host["trajectory_length"][i])
+        out = {}
+        for k, v in self._host.items():
+            if k == "trajectory_length":
+                out[k] = L
+            elif k in self._FULL:
+                out[k] = v[i]
+            else:
+                out[k] = v[i, :L]
+        return out
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
 class ResetNeeded(RuntimeError):
     """step() before reset() (gymnasium's OrderEnforcing wrapper, error.ResetNeeded [EXT-M])."""
 
@@ -99,6 +153,8 @@ class BlackBoxVectorEnv:
         self.meta = meta
         self.num_envs = int(num_envs)
         self.info_level = meta["verbose"] if info_level is None else int(info_level)
+        if self.info_level not in (0, 1, 2):
+            raise ValueError("info_level must be 0, 1 or 2")
         self.autoreset = bool(autoreset)
         self.seed_offset = int(seed_offset)
         self._needs_reset = True
@@ -142,46 +198,44 @@ class BlackBoxVectorEnv:
 
     # ------------------------------------------------------------------ gymnasium-style API
     def reset(self, *, seed=None, options=None):
-        N = self.num_envs
-        obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
-        seeds = None
-        if seed is not None:
-            if isinstance(seed, (list, tuple, np.ndarray, torch.Tensor)):
-                s = torch.as_tensor(np.asarray(seed, dtype=np.uint64).astype(np.int64), device=self.device)
-            else:
-                s = torch.arange(N, dtype=torch.int64, device=self.device) + (int(seed) + self.seed_offset)
-            seeds = s.contiguous()
-        mask = None
-        if options and options.get("reset_mask") is not None:
-            mask = torch.as_tensor(options["reset_mask"], dtype=torch.uint8, device=self.device).contiguous()
-        _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), _ptr(mask), _ptr(obs), self._eng.stream()))
-        self._needs_reset = False
+        """seed: int (env i gets seed + seed_offset + i) or one seed per env; options:
+        'random_start' (base_reacher.py:77-80) and 'reset_mask' ([N] bool: reset only those envs,
+        the others' rows of obs hold their current observation)."""
+        obs = torch.empty((self.num_envs, self.out_dim), dtype=torch.float32, device=self.device)
+        _reset_engine(self, seed, options, obs)
         return obs, {}
 
     def _info_buffers(self):
-        """verbose-2 per-step arrays.  The device writes them time-major ([T, N, ...], coalesced
-        across envs, include/fgx.h fgx_info); the caller sees [N, T, ...] transposed views."""
-        if self.info_level < 2:
+        """Per-step info arrays of the info level (module docstring).  The device writes them
+        time-major ([T, N, ...], coalesced across envs, include/fgx.h fgx_info); the caller sees
+        [N, T, ...] transposed views.  A generic reward_aggregation also needs step_rewards."""
+        generic_agg = callable(self.meta["reward_aggregation"])
+        if self.info_level == 0 and not generic_agg:
             return None, {}
         N, T, n, dev = self.num_envs, self.T, self.dof, self.device
         # every row is written by the kernel (NaN / 0 after trajectory_length): no fill here
         e = lambda *shape, dt=torch.float32: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
-        raw = dict(positions=e(T, N, n), velocities=e(T, N, n), step_actions=e(T, N, n, dt=torch.float64),
-                   step_observations=e(T, N, self.full_dim), step_rewards=e(T, N, dt=torch.float64))
+        raw = {}
         info = _lib.FgxInfo()
-        info.positions, info.velocities = raw["positions"].data_ptr(), raw["velocities"].data_ptr()
-        info.step_actions, info.step_obs = raw["step_actions"].data_ptr(), raw["step_observations"].data_ptr()
-        info.step_rewards = raw["step_rewards"].data_ptr()
-        if self.meta["kind"] in ("hole", "via"):
-            raw["is_collided"] = e(T, N, dt=torch.uint8)
-            raw["is_success"] = e(T, N, dt=torch.uint8)
-            raw["end_effector"] = e(T, N, 2, dt=torch.float64)
-            info.is_collided, info.is_success = raw["is_collided"].data_ptr(), raw["is_success"].data_ptr()
-            info.end_effector = raw["end_effector"].data_ptr()
-        else:
-            raw["reward_dist"] = e(T, N, dt=torch.float64)
-            raw["reward_ctrl"] = e(T, N, dt=torch.float64)
-            info.reward_dist, info.reward_ctrl = raw["reward_dist"].data_ptr(), raw["reward_ctrl"].data_ptr()
+        if self.info_level >= 2:
+            raw.update(positions=e(T, N, n), velocities=e(T, N, n), step_actions=e(T, N, n, dt=torch.float64),
+                       step_observations=e(T, N, self.full_dim))
+            info.positions, info.velocities = raw["positions"].data_ptr(), raw["velocities"].data_ptr()
+            info.step_actions, info.step_obs = raw["step_actions"].data_ptr(), raw["step_observations"].data_ptr()
+        if self.info_level >= 2 or generic_agg:
+            raw["step_rewards"] = e(T, N, dt=torch.float64)
+            info.step_rewards = raw["step_rewards"].data_ptr()
+        if self.info_level >= 1:
+            if self.meta["kind"] in ("hole", "via"):
+                raw["is_collided"] = e(T, N, dt=torch.uint8)
+                raw["is_success"] = e(T, N, dt=torch.uint8)
+                raw["end_effector"] = e(T, N, 2, dt=torch.float64)
+                info.is_collided, info.is_success = raw["is_collided"].data_ptr(), raw["is_success"].data_ptr()
+                info.end_effector = raw["end_effector"].data_ptr()
+            else:
+                raw["reward_dist"] = e(T, N, dt=torch.float64)
+                raw["reward_ctrl"] = e(T, N, dt=torch.float64)
+                info.reward_dist, info.reward_ctrl = raw["reward_dist"].data_ptr(), raw["reward_ctrl"].data_ptr()
         return info, {k: v.transpose(0, 1) for k, v in raw.items()}
 
     def _check_actions(self, actions):
@@ -227,22 +281,46 @@ class BlackBoxVectorEnv:
                                                _ptr(tr), _ptr(tl), _ptr(fobs),
                                                ctypes.byref(info_s) if info_s is not None else None,
                                                int(self.autoreset), self._eng.stream()))
-        if bufs:
+        if self.info_level >= 2:
             bufs["positions"], bufs["velocities"] = p, v
         return self._package(obs, ret, te, tr, tl, fobs, bufs)
 
     def _package(self, obs, ret, te, tr, tl, fobs, bufs):
+        """(obs, return, terminated, truncated, info) as gymnasium 0.29's SyncVectorEnv assembles
+        them from the envs' BlackBoxWrapper.step results (black_box_wrapper.py:241-253).
+
+        info holds every per-env key for all envs, with gymnasium's '_key' masks marking the envs
+        whose step info gymnasium would report there (those that did not finish: a finished env's
+        step info moves to info['final_info'][i], its last observation to
+        info['final_observation'][i])."""
         term, trunc = te.bool(), tr.bool()
-        if self.meta["reward_aggregation"] == "mean":
+        agg = self.meta["reward_aggregation"]
+        if agg == "mean":
             ret = ret / tl.to(torch.float64)
-        info = {"trajectory_length": tl}
+        elif callable(agg):   # any callable on rewards[:t+1] (black_box_wrapper.py:252), host numpy
+            rew = bufs["step_rewards"].detach().cpu().numpy()
+            L = tl.detach().cpu().numpy()
+            ret = torch.tensor([float(agg(rew[i, :L[i]])) for i in range(self.num_envs)], dtype=torch.float64,
+                               device=self.device)
+            if self.info_level < 2:
+                bufs = {k: v for k, v in bufs.items() if k != "step_rewards"}
+        per_env = {"trajectory_length": tl}
+        per_env.update(bufs)
+        info = dict(per_env)
         if self.autoreset:
             done = term | trunc
+            keep = ~done
+            for k in per_env:
+                info["_" + k] = keep
             info["final_observation"] = fobs
             info["_final_observation"] = done
+            info["final_info"] = FinalInfo(done, per_env)
+            info["_final_info"] = done
         else:
+            ones = torch.ones_like(term)
+            for k in per_env:
+                info["_" + k] = ones
             info["final_observation"] = fobs
-        info.update(bufs)
         return obs, ret, term, trunc, info
 
     def trajectory(self, actions):
@@ -329,13 +407,8 @@ class StepVectorEnv:
         self.single_action_space = Box(-bound, bound, (self.dof,), np.float32)
 
     def reset(self, *, seed=None, options=None):
-        N = self.num_envs
-        obs = torch.empty((N, self.obs_dim), dtype=torch.float32, device=self.device)
-        seeds = None
-        if seed is not None:
-            seeds = (torch.arange(N, dtype=torch.int64, device=self.device) + (int(seed) + self.seed_offset)).contiguous()
-        _lib.check(self._eng.lib.fgx_reset(self._eng.h, _ptr(seeds), None, _ptr(obs), self._eng.stream()))
-        self._needs_reset = False
+        obs = torch.empty((self.num_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+        _reset_engine(self, seed, options, obs)
         return obs, {}
 
     def step(self, actions):
@@ -352,7 +425,11 @@ class StepVectorEnv:
         _lib.check(self._eng.lib.fgx_step_raw(self._eng.h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(te), _ptr(tr),
                                               _ptr(fobs), int(self.autoreset), self._eng.stream()))
         term, trunc = te.bool(), tr.bool()
-        info = {"final_observation": fobs, "_final_observation": term | trunc}
+        done = term | trunc
+        info = {"final_observation": fobs, "_final_observation": done}
+        if self.autoreset:
+            info["final_info"] = FinalInfo(done, {})
+            info["_final_info"] = done
         return obs, rew, term, trunc, info
 
     def get_state(self):
@@ -360,6 +437,32 @@ class StepVectorEnv:
 
     def close(self):
         self._eng.close()
+
+
+def _reset_engine(env, seed, options, obs):
+    """fgx_reset for either env class: seeds (int -> seed + seed_offset + i, or one per env),
+    options 'random_start' / 'reset_mask' (checked against num_envs before any device read)."""
+    N, dev = env.num_envs, env.device
+    seeds = None
+    if seed is not None:
+        if isinstance(seed, (list, tuple, np.ndarray, torch.Tensor)):
+            arr = np.asarray(seed.cpu() if isinstance(seed, torch.Tensor) else seed).reshape(-1)
+            if arr.shape[0] != N:
+                raise ValueError(f"seed list has {arr.shape[0]} entries for {N} envs")
+            seeds = torch.as_tensor(arr.astype(np.uint64).astype(np.int64), device=dev)
+        else:
+            seeds = torch.arange(N, dtype=torch.int64, device=dev) + (int(seed) + env.seed_offset)
+        seeds = seeds.contiguous()
+    options = options or {}
+    mask = None
+    if options.get("reset_mask") is not None:
+        mask = torch.as_tensor(options["reset_mask"], device=dev).reshape(-1).to(torch.uint8).contiguous()
+        if mask.numel() != N:
+            raise ValueError(f"reset_mask has {mask.numel()} entries for {N} envs")
+    rs = options.get("random_start")
+    rs = -1 if rs is None else int(bool(rs))
+    _lib.check(env._eng.lib.fgx_reset(env._eng.h, _ptr(seeds), _ptr(mask), rs, _ptr(obs), env._eng.stream()))
+    env._needs_reset = False
 
 
 def math_isnan(x):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 4
+#define FGX_ABI_VERSION 5
 
 /* error codes */
 #define FGX_OK 0
@@ -128,7 +128,8 @@ typedef struct fgx_config {
   double tau_bound_lo, tau_bound_hi;     /* make_env_helpers.py:118-122 ([2 dt, duration])  */
   double delay_bound_lo, delay_bound_hi; /* make_env_helpers.py:124-126 ([0, duration-2dt]) */
   double via_x, via_y;          /* ViaPointReacher via_target (NaN = sampled, viapoint_reacher.py:60-66) */
-  double target_x, target_y;    /* ViaPointReacher target     (NaN = sampled, :68-74)      */
+  double target_x, target_y;    /* ViaPointReacher / SimpleReacher target (NaN = sampled;
+                                   viapoint_reacher.py:68-74, simple_reacher.py:85-96)        */
   /* ---- ABI 3: replanning schedule as a clause program (sched_n == 0 and replan_period > 0
    * is the single clause EVERY(replan_period)) */
   int32_t sched_n;
@@ -169,6 +170,8 @@ typedef struct fgx_info {
 
 const char* fgx_last_error(void);
 int fgx_abi_version(void);
+/* Hash of the sources (csrc/, include/fgx.h) this library was built from (build provenance). */
+const char* fgx_build_id(void);
 
 int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle);
 int fgx_destroy(void* handle);
@@ -176,8 +179,12 @@ int fgx_get_dims(void* handle, fgx_dims* out);
 
 /* Reset the envs where mask[i] != 0 (mask NULL = all).  seeds: device u64 [N] or NULL
  * (NULL = continue each env's own PCG64 stream, i.e. reset() without a seed).
- * obs_out: [N, out_obs_dim] f32; rows of envs not reset are left untouched. */
-int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, float* obs_out, void* stream);
+ * random_start: -1 = the env's constructor setting, 0 / 1 = reset(options={'random_start': ...})
+ * (base_reacher.py:77-86; a non-random reset restores the env's last start angle).
+ * obs_out: [N, out_obs_dim] f32 (NULL ok); rows of envs not reset receive their current
+ * observation.  seeds and mask, when given, must hold N entries. */
+int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, int32_t random_start, float* obs_out,
+              void* stream);
 
 /* One black-box step for all N envs: MP parameters params [N, n_params] f32 ->
  * obs [N, out_obs_dim] f32 (already auto-reset for finished envs), ret [N] f64 (episode-segment

@@ -63,12 +63,12 @@ class BatchedReacher:
             self.via = np.zeros((N, 2))
             self.allow_self, self.penalty = e0.allow_self, e0.penalty
 
-    def reset(self, idx, seeds=None):
+    def reset(self, idx, seeds=None, options=None):
         """Reset envs idx (list); returns obs [len(idx), obs_dim] f32."""
         out = []
         for j, i in enumerate(idx):
             e = self.envs[i]
-            o = e.reset(None if seeds is None else int(seeds[j]))
+            o = e.reset(None if seeds is None else int(seeds[j]), options)
             self.q[i] = e.q
             self.qd[i] = e.qd
             self.qd_f32[i] = False
@@ -290,8 +290,10 @@ class BatchedBB:
 
     def __init__(self, name, N, ctrl, mp_spec=None, traj_fn=None, replan_period=0,
                  max_planning_times=np.inf, condition_on_desired=False, info_level=0,
-                 time_aware=None, tables=None, env_kwargs=None, learned=None, schedule=None):
+                 time_aware=None, tables=None, env_kwargs=None, learned=None, schedule=None,
+                 reward_aggregation=np.sum):
         self.env = BatchedReacher(name, N, **(env_kwargs or {}))
+        self.reward_aggregation = reward_aggregation   # black_box_wrapper.py:252
         self.N = N
         self.ctrl = ctrl
         self.spec = mp_spec
@@ -333,17 +335,17 @@ class BatchedBB:
             o = o[:, self.env.mask]
         return o.astype(f32)
 
-    def _reset_idx(self, idx, seeds=None):
-        o = self.env.reset(idx, seeds)
+    def _reset_idx(self, idx, seeds=None, options=None):
+        o = self.env.reset(idx, seeds, options)
         self.traj_steps[idx] = 0
         self.plan_steps[idx] = 0
         self.has_cond[idx] = False
         return self.observation(self._full(o, np.zeros(len(idx))))
 
-    def reset(self, seed=None):
+    def reset(self, seed=None, options=None):
         idx = list(range(self.N))
         seeds = None if seed is None else [seed + i for i in idx]
-        return self._reset_idx(idx, seeds)
+        return self._reset_idx(idx, seeds, options)
 
     def step(self, params):
         env, N, n = self.env, self.N, self.env.n
@@ -409,7 +411,7 @@ class BatchedBB:
             if not np.any(act):
                 break
         self.traj_steps += tlen
-        ret = np.array([np.sum(rewards[i, :tlen[i]]) for i in range(N)])
+        ret = np.array([self.reward_aggregation(rewards[i, :tlen[i]]) for i in range(N)], np.float64)
         obs = self.observation(last_obs)
         final_obs = obs.copy()
         done = term | trunc
@@ -422,3 +424,16 @@ class BatchedBB:
                             step_observations=obs_log, step_rewards=rewards)
             out_info.update(info_log)
         return obs, ret, term, trunc, out_info
+
+
+def run_chunk(args):
+    """Flags / lengths / returns of global envs [lo, hi) (env i seeded i) over a list of BB-step
+    parameter blocks: the unit of work of the tests' process-parallel full-batch checks."""
+    name, ctrl, spec, tables, kw, lo, hi, plist = args
+    ob = BatchedBB(name, hi - lo, ctrl, mp_spec=spec, tables=tables, **kw)
+    ob._reset_idx(list(range(hi - lo)), list(range(lo, hi)))
+    out = []
+    for p in plist:
+        _, r_ret, r_te, r_tr, r_info = ob.step(p)
+        out.append((r_info["trajectory_length"], r_te, r_tr, r_ret))
+    return lo, out

@@ -26,6 +26,8 @@ Outputs (small .npz files):
     resets.npz, step_based.npz, bb_simple.npz, bb_long.npz, bb_hole_vel.npz,
     bb_hole_pd.npz, bb_replan.npz                     ("base")
     variants.npz  ViaPointReacher + HoleReacher rew_fct vel_acc / unbounded ("variants")
+    options.npz   reset(options={'random_start'}), SimpleReacher(target=...), reward_aggregation
+                  callables ("options")
 
 Run:  python tests/golden/make_golden.py [base] [variants]   (needs /root/reference; not on the GPU box)
 """
@@ -203,6 +205,9 @@ class _Spec:
     max_episode_steps = 200
 
 
+TARGET = (1.25, -0.5)   # fixed SimpleReacher target of the "options" fixtures
+
+
 # registered kwargs: envs/__init__.py:57-65 (SimpleReacher), :658-666 (Long), :682-698 (Hole)
 def make_raw(kind):
     if kind == "simple":
@@ -216,6 +221,8 @@ def make_raw(kind):
                              hole_x=None, collision_penalty=100, rew_fct=rew)
     elif kind == "via":   # envs/__init__.py:669-679
         env = ViaPointReacherEnv(n_links=5, allow_self_collision=False, collision_penalty=1000)
+    elif kind.startswith("target"):   # SimpleReacherEnv(target=...) (simple_reacher.py:19,93-94)
+        env = SimpleReacherEnv(n_links=2 if kind == "target" else 5, target=TARGET)
     else:
         raise ValueError(kind)
     env.spec = _Spec()
@@ -346,7 +353,7 @@ def gen_step_based():
 
 
 # ----------------------------------------------------------------------------- (iii)/(iv) BB
-def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True, out_dict=None):
+def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True, out_dict=None, bb_kw=None):
     """E envs, reset(seed=100+i), n_bb BB steps each with autoreset; stub MP tables per (env, bb)."""
     rng = np.random.default_rng(4321)
     wrap = {"via": VPMPWrapper}.get(kind, HRMPWrapper if kind.startswith("hole") else SRMPWrapper)
@@ -362,7 +369,7 @@ def run_bb(name, kind, controller, E, n_bb, table_fn, replan=None, ctx=True, out
         n_rows = 400 if replan is not None else 200
         pos_t, vel_t = table_fn(rng, n_rows, dof)
         tg = StubTrajGen(dof * 5, pos_t, vel_t)
-        kw = {}
+        kw = dict(bb_kw or {})
         if replan is not None:
             kw["replanning_schedule"] = replan
         bb = BlackBoxWrapper(env, trajectory_generator=tg, tracking_controller=controller,
@@ -486,14 +493,71 @@ def gen_variants():
     np.savez_compressed(os.path.join(OUT, "variants.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- (vii) options
+RESET_SEQ = [("seed", None), (None, {"random_start": False}), (None, None), (None, {"random_start": "flip"}),
+             (None, {"random_start": False}), (None, None), ("seed", {"random_start": False})]
+
+
+def gen_options():
+    """reset(options={'random_start': ...}) sequences (base_reacher.py:77-86: a non-random reset
+    restores _start_pos, which a random one replaces), SimpleReacher(target=...) resets and
+    step-based rollouts, and BB steps with reward_aggregation callables other than np.sum
+    (black_box_wrapper.py:252; test/test_black_box.py:139-150 uses np.median and a lambda)."""
+    out = {}
+    for kind in ("simple", "long", "hole", "via", "target", "target_long"):
+        rec = {k: [] for k in ("q0", "goal", "obs")}
+        for s in range(16):
+            env = make_raw(kind)
+            u = env.unwrapped
+            q0, goal, obs = [], [], []
+            for sd, opt in RESET_SEQ:
+                if opt is not None and opt.get("random_start") == "flip":
+                    opt = {"random_start": not u.random_start}
+                o, _ = env.reset(seed=s if sd else None, options=opt)
+                q0.append(u._joint_angles.copy()); goal.append(np.array(u._goal, np.float64)); obs.append(o)
+            rec["q0"].append(q0); rec["goal"].append(goal); rec["obs"].append(obs)
+        out.update({f"{kind}_reset_{k}": np.array(v) for k, v in rec.items()})
+    for kind, E, dof in (("target", 4, 2), ("target_long", 3, 5)):
+        rng = np.random.default_rng(5)
+        acts = rng.uniform(-100, 100, (60, E, dof)).astype(np.float32)
+        envs = [make_raw(kind) for _ in range(E)]
+        out[f"{kind}_obs0"] = np.array([e.reset(seed=i)[0] for i, e in enumerate(envs)])
+        O, R = [], []
+        for t in range(60):
+            o_t, r_t = [], []
+            for i, e in enumerate(envs):
+                o, r, te, tr, _ = e.step(acts[t, i])
+                o_t.append(o); r_t.append(float(r))
+            O.append(o_t); R.append(r_t)
+        out[f"{kind}_actions"] = acts
+        out[f"{kind}_obs"] = np.array(O, dtype=np.float32)
+        out[f"{kind}_rew"] = np.array(R)
+
+    def simple_tab(rng, n, dof):
+        return smooth_tables(rng, n, dof, 1.0, 3.0)
+
+    def hole_pd_tab(rng, n, dof):
+        off = rng.uniform(-3.5, 3.5, dof)
+        off[0] = rng.uniform(0.0, np.pi)
+        return smooth_tables(rng, n, dof, 0.6, 1.0, offset=off)
+
+    run_bb("aggmedian", "long", PDController(0.6, 0.075), 4, 2, simple_tab, out_dict=out,
+           bb_kw={"reward_aggregation": np.median})
+    run_bb("aggeven", "hole", PDController(1.0, 0.1), 6, 2, hole_pd_tab, out_dict=out,
+           bb_kw={"reward_aggregation": lambda x: np.mean(x[::2])})
+    np.savez_compressed(os.path.join(OUT, "options.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["base", "variants"]
+    which = sys.argv[1:] or ["base", "variants", "options"]
     if "base" in which:
         gen_resets()
         gen_step_based()
         gen_bb()
     if "variants" in which:
         gen_variants()
+    if "options" in which:
+        gen_options()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -1,0 +1,102 @@
+"""Multi-rank path on the device.
+
+* Two gloo ranks sharing cuda:0 (the 1-GPU rehearsal of one-process-per-GPU) each run their
+  contiguous shard of a 2N-env batch — fgx.make(..., seed_offset=rank * N) and the rank's rows of
+  the global parameter matrix — and all-gather returns, flags, lengths and observations.  The
+  gathered result must equal a single-process 2N-env run BIT-EXACTLY: envs are independent and
+  seeded by global index (reference usage: examples/examples_general.py:68-110, AsyncVectorEnv
+  over independent envs).
+* bench.py's distributed leg under torch.distributed.run with 2 ranks (strong scaling: the
+  global batch split over the ranks) prints one well-formed JSON line.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import fancy_gym_crowd_amd as fgx
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV_ID = "fancy_ProMP/LongSimpleReacher-v0"
+N, N_BB, WORLD = 384, 3, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _params(P):
+    rng = np.random.default_rng(77)
+    return [rng.standard_normal((N * WORLD, P), dtype=np.float32) for _ in range(N_BB)]
+
+
+def _rank_main(rank, port, out_path):
+    import torch.distributed as dist
+
+    from fancy_gym_crowd_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.cuda.set_device(0)
+    lo, hi = shard.shard_range(N, rank, WORLD)
+    env = fgx.make(ENV_ID, num_envs=N, device="cuda:0", seed_offset=lo, info_level=0)
+    env.reset(seed=0)
+    rec = {k: [] for k in ("ret", "te", "tr", "tl", "obs")}
+    for p in _params(env.n_params):
+        obs, ret, te, tr, info = env.step(torch.from_numpy(shard.shard_rows(p, rank, WORLD).copy()).cuda())
+        for k, v in (("ret", ret), ("te", te), ("tr", tr), ("tl", info["trajectory_length"]), ("obs", obs)):
+            v = v.cpu().contiguous()
+            parts = [torch.empty_like(v) for _ in range(WORLD)]
+            dist.all_gather(parts, v)
+            rec[k].append(torch.cat(parts).numpy())
+    if rank == 0:
+        np.savez(out_path, **{k: np.stack(v) for k, v in rec.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_equal_single_process_bit_exact():
+    port = _free_port()
+    out = os.path.join(tempfile.mkdtemp(prefix="fgx_dist_"), "r0.npz")
+    ctx = mp.get_context("spawn")   # fresh interpreters; this process may already hold the GPU
+    procs = [ctx.Process(target=_rank_main, args=(r, port, out)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0, p.exitcode
+    got = np.load(out)
+    env = fgx.make(ENV_ID, num_envs=N * WORLD, device="cuda:0", info_level=0)
+    env.reset(seed=0)
+    for b, p in enumerate(_params(env.n_params)):
+        obs, ret, te, tr, info = env.step(torch.from_numpy(p).cuda())
+        np.testing.assert_array_equal(got["ret"][b], ret.cpu().numpy())
+        np.testing.assert_array_equal(got["te"][b], te.cpu().numpy())
+        np.testing.assert_array_equal(got["tr"][b], tr.cpu().numpy())
+        np.testing.assert_array_equal(got["tl"][b], info["trajectory_length"].cpu().numpy())
+        np.testing.assert_array_equal(got["obs"][b], obs.cpu().numpy())
+
+
+def test_bench_distributed_leg_two_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--global-envs", "2048", "--no-weak"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_envs"] == 2048 and d["config"]["envs_per_gpu"] == 1024
+    assert d["value"] > 0 and d["steps"] == 3

@@ -82,7 +82,7 @@ def _same(a, b):
 @pytest.mark.parametrize("ci", range(len(CASES)))
 def test_jp_equals_classic_kernel(ci):
     env_id, over, N, n_bb = CASES[ci]
-    probe = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+    probe = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     rng = np.random.default_rng(40 + ci)
     params = [rng.standard_normal((N, probe.n_params), dtype=np.float32) for _ in range(n_bb)]
     _same(_run(env_id, over, N, n_bb, "jp", 300 + ci, params),
@@ -93,7 +93,7 @@ def test_jp_equals_classic_nan_and_restored_steps():
     """NaN / inf / huge parameters (np.clip NaN propagation, clip at the torque bound) and a
     restored state with every env at a different step (segments of every length 1..200)."""
     env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 320
-    probe = fgx.make(env_id, num_envs=N, device=DEV)
+    probe = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
     rng = np.random.default_rng(5)
     p = rng.standard_normal((2, N, probe.n_params)).astype(np.float32)
     p[0, 3, 4] = np.nan
@@ -115,7 +115,7 @@ def test_jp_vs_oracle_desynchronised():
     """jp alone (selected by default at this size) against the oracle with lanes at different env
     steps (set_state)."""
     env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 200
-    env = fgx.make(env_id, num_envs=N, device=DEV)
+    env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
     spec = spec_of(env)
     ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
                            tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))

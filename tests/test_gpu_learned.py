@@ -109,7 +109,7 @@ def test_learn_delay_structure_on_device(delay):
 @pytest.mark.parametrize("mp", ["ProMP", "DMP"])
 def test_sub_trajectory_lengths_on_device(mp):
     """test_replanning_sequencing.py:99-107: length == round(tau / dt) unless the episode ends."""
-    env = fgx.make(f"fancy_{mp}/SimpleReacher-v0", num_envs=64, device=DEV,
+    env = fgx.make(f"fancy_{mp}/SimpleReacher-v0", num_envs=64, device=DEV, info_level=0,
                    mp_config_override={"black_box_kwargs": {"learn_sub_trajectories": True}})
     env.reset(seed=1)
     rng = np.random.default_rng(3)

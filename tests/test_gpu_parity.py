@@ -362,7 +362,7 @@ def test_step_based_golden():
 def test_large_batch_invariants():
     """BASELINE metric size: properties that do not need the oracle."""
     N = 65536
-    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV)
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, info_level=0)
     env.reset(seed=0)
     params = torch.randn((N, env.n_params), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
     obs, ret, te, tr, info = env.step(params)
@@ -370,7 +370,7 @@ def test_large_batch_invariants():
     assert bool(tr.all()) and not bool(te.any())
     assert bool(torch.isfinite(ret).all()) and bool((ret <= 0).all())
     # the same seed and params give the same result (determinism, test/utils.py:72-88)
-    env2 = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV)
+    env2 = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, info_level=0)
     env2.reset(seed=0)
     obs2, ret2, te2, tr2, _ = env2.step(params)
     assert torch.equal(ret, ret2) and torch.equal(obs, obs2)
@@ -387,7 +387,7 @@ def test_large_batch_invariants():
 
 def test_reset_mask_and_determinism():
     N = 256
-    env = fgx.make("fancy_ProMP/HoleReacher-v0", num_envs=N, device=DEV)
+    env = fgx.make("fancy_ProMP/HoleReacher-v0", num_envs=N, device=DEV, info_level=0)
     env.reset(seed=9)
     before = {k: np_(v) for k, v in env.get_state().items()}
     mask = np.zeros(N, np.uint8)
@@ -415,7 +415,7 @@ def test_per_joint_pd_gains():
     """PDController with one gain per joint (tuple gains broadcast against the joint arrays)."""
     over = {"controller_kwargs": {"p_gains": (0.5, 0.9, 1.3, 0.7, 2.0), "d_gains": [0.05, 0.1, 0.2, 0.02, 0.3]}}
     N = 256
-    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, mp_config_override=over)
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     spec = spec_of(env)
     ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
                            tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
@@ -438,7 +438,7 @@ def test_generic_basis_count(ci):
     env_id, nb = NB_CASES[ci]
     over = {"basis_generator_kwargs": {"num_basis": nb}}
     N = 192
-    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+    env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     spec = spec_of(env)
     assert spec.n_basis == nb and env.n_params == spec.n_params
     tabs = split_tables(spec, np_(env.tables()))
@@ -498,7 +498,7 @@ def test_wall_collision_randomised_raw_steps(name, kw):
 def test_set_state_then_step_matches_oracle():
     """fgx_set_state (checkpoint restore): a BB step from an arbitrary restored state."""
     N = 192
-    env = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=N, device=DEV)
+    env = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=N, device=DEV, info_level=0)
     env.reset(seed=17)
     rng = np.random.default_rng(2)
     st = {k: np_(v) for k, v in env.get_state().items()}
@@ -531,9 +531,9 @@ def test_no_autoreset_and_mean_aggregation():
     reward_aggregation=np.mean divides the pairwise sum by the trajectory length."""
     N = 128
     over = {"black_box_kwargs": {"reward_aggregation": np.mean}}
-    env = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV, autoreset=False,
+    env = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV, info_level=0, autoreset=False,
                    mp_config_override=over)
-    ref = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV)
+    ref = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV, info_level=0)
     env.reset(seed=5)
     ref.reset(seed=5)
     params = torch.from_numpy(np.random.default_rng(0).standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)

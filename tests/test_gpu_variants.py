@@ -31,7 +31,7 @@ def g():
 
 
 def test_via_reset_golden(g):
-    env = fgx.make("fancy_ProMP/ViaPointReacher-v0", num_envs=64, device=DEV)
+    env = fgx.make("fancy_ProMP/ViaPointReacher-v0", num_envs=64, device=DEV, info_level=0)
     obs, _ = env.reset(seed=0)
     close(np_(obs), g["viareset_obs"][:, np.array([False] * 15 + [True] * 4 + [False])])
     st = env.get_state()

@@ -25,7 +25,7 @@ WS_CASES = CASES + [
 @pytest.mark.parametrize("ci", range(len(WS_CASES)))
 def test_ws_equals_classic_kernel(ci):
     env_id, over, N, n_bb = WS_CASES[ci]
-    probe = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+    probe = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     rng = np.random.default_rng(70 + ci)
     params = [rng.standard_normal((N, probe.n_params), dtype=np.float32) for _ in range(n_bb)]
     _same(_run(env_id, over, N, n_bb, "ws", 500 + ci, params),
@@ -34,7 +34,7 @@ def test_ws_equals_classic_kernel(ci):
 
 def test_ws_equals_classic_nan_and_restored_steps():
     env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 1000
-    probe = fgx.make(env_id, num_envs=N, device=DEV)
+    probe = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
     rng = np.random.default_rng(6)
     p = rng.standard_normal((3, N, probe.n_params)).astype(np.float32)
     p[0, 3, 4] = np.nan
@@ -61,5 +61,5 @@ def test_episode_kernel_selection():
              ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_ws"),         # config 5 shard
              ("fancy_ProDMP/HoleReacher-v0", None, 4096, 0, "k_episode")]
     for env_id, over, N, lvl, want in cases:
-        env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+        env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
         assert env.episode_kernel(lvl) == want, (env_id, N, lvl)

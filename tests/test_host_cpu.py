@@ -18,9 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _ensure_built():
-    if not os.path.exists(_lib.LIB_PATH):
-        from fancy_gym_crowd_amd import _build
-        _build.build()
+    from fancy_gym_crowd_amd import _build
+    _build.build()   # no-op when the library's build id matches the sources
 
 
 def test_library_exports_every_declared_symbol():
@@ -44,6 +43,9 @@ def test_library_loads_and_reports_abi():
     _ensure_built()
     lib = _lib.load()
     assert lib.fgx_abi_version() == _lib.FGX_ABI_VERSION
+    # build provenance: the loaded library was compiled from exactly the tracked sources
+    from fancy_gym_crowd_amd import _build
+    assert lib.fgx_build_id().decode() == _build.source_hash() == _build.built_id()
     # argument validation happens before any device work
     cfg = _lib.FgxConfig()
     cfg.abi_version = 999

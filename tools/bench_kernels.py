@@ -42,7 +42,7 @@ def timed(fn, reps=20, warm=3):
 
 
 def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
-    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over, **(env_kwargs or {}))
+    env = fgx.make(env_id, num_envs=N, device=dev, info_level=0, mp_config_override=over, **(env_kwargs or {}))
     env.reset(seed=0)
     P = env.n_params
     params = torch.from_numpy(np.random.default_rng(1234).standard_normal((N, P), dtype=np.float32)).to(dev)
@@ -65,7 +65,7 @@ def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
 
 def trajectory(env_id, N, force_valu=False):
     over = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}} if force_valu else None
-    env = fgx.make(env_id, num_envs=N, device=dev, mp_config_override=over)
+    env = fgx.make(env_id, num_envs=N, device=dev, info_level=0, mp_config_override=over)
     env.reset(seed=0)
     params = torch.randn((N, env.n_params), device=dev)
     T, n = env.T, env.dof
@@ -84,7 +84,7 @@ def trajectory(env_id, N, force_valu=False):
 
 
 def step_raw(env_id, N):
-    env = fgx.make(env_id, num_envs=N, device=dev)
+    env = fgx.make(env_id, num_envs=N, device=dev, info_level=0)
     env.reset(seed=0)
     n = env.dof
     a = (torch.rand((N, n), device=dev) * 2 - 1) * 10

@@ -10,7 +10,7 @@ import fancy_gym_crowd_amd as fgx  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 dev = torch.device("cuda", 0)
-env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=dev)
+env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=dev, info_level=0)
 env.reset(seed=0)
 params = torch.randn((N, env.n_params), device=dev)
 obs = torch.empty((N, env.out_dim), device=dev)
