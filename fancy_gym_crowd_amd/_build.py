@@ -67,6 +67,27 @@ def _compile(src, bid, verbose):
     return obj
 
 
+def build_variant(out, defines=(), verbose=False):
+    """A diagnostics build of the same sources with extra -D flags (e.g. FGX_STAMPS) into `out`
+    (loaded with FGX_LIB; its build id is not checked).  Never the in-tree library."""
+    objdir = os.path.join(OBJDIR, "variant_" + "_".join(d.split("=")[0] for d in defines))
+    os.makedirs(objdir, exist_ok=True)
+    bid = source_hash() + "+" + ",".join(defines)
+
+    def one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [_hipcc(), *FLAGS, *[f"-D{d}" for d in defines], f'-DFGX_BUILD_ID="{bid}"', "-I", INC, "-c",
+               os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+    with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(one, SOURCES))
+    subprocess.run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out], check=True)
+    return out
+
+
 def build(force=False, verbose=True):
     bid = source_hash()
     if not force and built_id() == bid:

@@ -429,6 +429,9 @@ int fgx_reset(void* handle, const uint64_t* seeds, const uint8_t* mask, int32_t 
   return launch_reset(*h, seeds, mask, random_start, obs_out, (hipStream_t)stream);
 }
 
+#ifdef FGX_STAMPS
+static unsigned long long* g_stamps = nullptr;
+#endif
 static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, int32_t* tlen, float* fobs,
                             const fgx_info* info, int32_t autoreset) {
   Outputs o;
@@ -448,8 +451,22 @@ static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, i
     o.reward_ctrl = info->reward_ctrl;
     o.inner_steps = (long long*)info->inner_steps;
   }
+#ifdef FGX_STAMPS
+  static unsigned long long* stamps = nullptr;   // diagnostics build only (tools/stamps.py)
+  if (!stamps && hipMalloc(&stamps, 16384 * 8 * sizeof(unsigned long long)) != hipSuccess) stamps = nullptr;
+  o.stamps = stamps;
+  g_stamps = stamps;
+#endif
   return o;
 }
+
+#ifdef FGX_STAMPS
+// Copies the section clocks of the last episode launch (n values) to host memory.
+extern "C" int fgx_dbg_stamps(unsigned long long* host, int n) {
+  if (!g_stamps) return -1;
+  return hipMemcpy(host, g_stamps, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t* terminated, uint8_t* truncated,
              int32_t* traj_len, float* final_obs, const fgx_info* info, int32_t autoreset, void* stream) {

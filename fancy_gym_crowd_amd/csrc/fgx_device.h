@@ -15,6 +15,9 @@ namespace fgx {
 
 // two f32 lanes per register pair: v_pk_{fma,mul,add}_f32 operands
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// read-only table memory in the constant address space: a wave-uniform address is loaded with
+// s_load into SGPRs (the scalar cache), not per lane through LDS / VMEM
+typedef const float __attribute__((address_space(4)))* cfloat_ptr;
 
 constexpr int kMaxLinks = 8;
 constexpr int kMaxObs = 3 * kMaxLinks + 5;
@@ -102,7 +105,24 @@ struct Outputs {
   double* reward_ctrl;
   long long* inner_steps;
   int autoreset;
+#ifdef FGX_STAMPS
+  unsigned long long* stamps;   // diagnostics build only: per-wave section clocks (tools/stamps.py)
+#endif
 };
+
+// Section clocks of one wave (diagnostics build, -DFGX_STAMPS): lane 0 of wave w stores the shader
+// clock (s_memtime) at point i to stamps[w * 8 + i] with an ordinary vector store.
+#ifdef FGX_STAMPS
+#define FGX_STAMP(o, e, i)                                                                \
+  do {                                                                                    \
+    const unsigned long long t_ = (i) >= 6 ? __builtin_amdgcn_s_memrealtime()             \
+                                           : __builtin_readcyclecounter();                \
+    if ((threadIdx.x & 63) == 0 && (o).stamps && ((e) >> 6) < 16384)                      \
+      (o).stamps[((e) >> 6) * 8 + (i)] = t_;                                              \
+  } while (0)
+#else
+#define FGX_STAMP(o, e, i) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------ wave reductions (all 64 lanes active)
 __device__ __forceinline__ int wave_min(int x) {

@@ -178,6 +178,8 @@ struct Traj {
   float y[NL], z[NL];      // DMP state
   float cur[NL], vprev[NL];// ProMP look-ahead (1 joint)
   const float* tab;        // row s0 of the basis table: plan sample k reads rows k + 1, k + 2
+  cfloat_ptr stab;         // the same row in global memory through the constant address space,
+                           // wave-uniform (fast blocks: rows land in SGPRs via s_load)
   int stride, T, nbr;
   float tau32, rtau32;
   // table row stride, compile-time for a fixed basis count (build_devcfg in fgx_api.hip): every
@@ -194,7 +196,8 @@ struct Traj {
   __device__ __forceinline__ float div_tau(float x) const { return DIVREF ? x / tau32 : div_rcp(x, tau32, rtau32); }
 
   // k-ordered f32 fma chain over the nb basis slots (== f32-input MFMA numerics)
-  __device__ __forceinline__ float chain(const float* row, const float* wd) const {
+  template <typename P>
+  __device__ __forceinline__ float chain(P row, const float* wd) const {
     float acc = 0.0f;
 #pragma unroll
     for (int j = 0; j < NBM; ++j)
@@ -202,7 +205,8 @@ struct Traj {
     return acc;
   }
   // the same chain on a joint pair (the table entry is broadcast to both halves)
-  __device__ __forceinline__ f32x2 chain2(const float* row, const f32x2* wd) const {
+  template <typename P>
+  __device__ __forceinline__ f32x2 chain2(P row, const f32x2* wd) const {
     f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < NBM; ++j)
@@ -289,13 +293,18 @@ struct Traj {
 
   // desired (pos, vel) of plan sample k (row s0 + k + 1); call with k = 0, 1, 2, ...
   // MID: the caller guarantees k < T - 1 (no last-sample branch)
-  template <bool MID = false>
+  // SC: read the rows through stab (k and stab wave-uniform)
+  template <bool MID = false, bool SC = false>
   __device__ __forceinline__ void at(const DevCfg& c, int k, float* pos, float* vel) {
-    const float* row = tab + (size_t)(k + 1) * str();
+    if constexpr (SC) at_rows<MID>(c, k, stab + (size_t)(k + 1) * str(), pos, vel);
+    else at_rows<MID>(c, k, tab + (size_t)(k + 1) * str(), pos, vel);
+  }
+  template <bool MID, typename RowPtr>
+  __device__ __forceinline__ void at_rows(const DevCfg& c, int k, RowPtr row, float* pos, float* vel) {
     const int n = nb();
     if (MP == MP_PROMP && PK) {
       if (MID || k < T - 1) {
-        const float* nrow = row + str();
+        const auto nrow = row + str();
         const float dti = row[n], rdt = row[n + 1];
 #pragma unroll
         for (int p = 0; p < NLP; ++p) {
@@ -320,7 +329,7 @@ struct Traj {
       }
     } else if (MP == MP_PROMP) {
       if (MID || k < T - 1) {
-        const float* nrow = row + str();
+        const auto nrow = row + str();
         const float dti = row[n], rdt = row[n + 1];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
@@ -640,6 +649,8 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= c.N) return;
   const int64_t N = c.N;
+  FGX_STAMP(o, e, 6);
+  FGX_STAMP(o, e, 0);
 
   Env<NL> v;
   load_env(c, s, e, v, ENV != ENV_SIMPLE);
@@ -678,6 +689,11 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   double* rew_row = ((ENV != ENV_SIMPLE || c.sched_state) && s.rew) ? s.rew + e : nullptr;
   bool term = false, trunc = false, stop = false;
   float pos[NL], vel[NL];
+  // fast blocks are software-pipelined: sample k's f64 controller / dynamics and the f32
+  // trajectory evaluation of sample k + 1 (into npos / nvel) form one scheduling region, so the
+  // independent f32 and f64 chains interleave and only one look-ahead sample is held in registers
+  float npos[NL], nvel[NL];
+  bool pre = false;   // npos / nvel hold the desired state of the next sample (wave-uniform)
   constexpr bool F32 = (CTRL != CTRL_PD);
 
   // One plan sample k: desired state -> controller -> clip -> env.step -> return / info.
@@ -695,7 +711,15 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
         vel[d] = dvel[(e * c.T + k) * NL + d];
       }
     } else if constexpr (J >= 0) {
-      tg.template at<true>(c, k, pos, vel);   // fast blocks end before the plan's last sample
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { pos[d] = npos[d]; vel[d] = nvel[d]; }
+      // fast samples k < lim2 <= T - 2: the look-ahead k + 1 is never the plan's last sample
+      tg.template at<true, true>(c, k + 1, npos, nvel);
+    } else if (pre) {
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { pos[d] = npos[d]; vel[d] = nvel[d]; }
+      pre = false;
     } else {
       tg.at(c, k, pos, vel);
     }
@@ -771,7 +795,142 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     return false;
   };
 
+  // Hand-levelled fast sample (SimpleReacher + ProMP on joint pairs + PD, the metric kernel).  One
+  // wave per SIMD issues from a single instruction stream, so every dependent f64 / f32 op must
+  // find independent work between itself and its producer.  The sample is written as levels
+  // separated by sched_barriers: each level holds one step of every joint's f64 chain (PD, clip,
+  // Euler, sum of squared actions) and one step of every pair's f32 trajectory chain for the NEXT
+  // sample (basis contraction, finite difference, div_rcp), so consecutive dependent instructions
+  // are >= 8 instructions apart.  The basis rows of the sample after next are loaded with scalar
+  // loads one region ahead.  Every operation is the one `sample` performs, in the same order per
+  // value: bit-identical results.
+  using TrajT = decltype(tg);
+  constexpr bool LV = !LOG && ENV == ENV_SIMPLE && MP == MP_PROMP && CTRL == CTRL_PD && NB > 0 && TrajT::PK;
+  constexpr int NBL = NB > 0 ? NB : 1;
+  constexpr int NLP = (NL + 1) / 2;
+  float rb_[NBL];         // basis row k + 3 (trajectory of sample k + 1: its next position)
+  float rdti = 0.0f, rrdt = 0.0f;   // dt and 1 / dt of row k + 2
+  int rmax = 0;           // last table row reachable through stab (wave-uniform)
+  auto lv_load = [&](int k) {   // rows for the region of sample k (clamped: never past the table)
+    const int rb = min(k + 3, rmax), rd = min(k + 2, rmax);
+#pragma unroll
+    for (int j = 0; j < NBL; ++j) rb_[j] = tg.stab[(size_t)rb * TrajT::KS + j];
+    rdti = tg.stab[(size_t)rd * TrajT::KS + NBL];
+    rrdt = tg.stab[(size_t)rd * TrajT::KS + NBL + 1];
+  };
+  auto lv_sample = [&](int k, auto Jtag, auto PHtag) {
+    constexpr int J = decltype(Jtag)::value;
+    constexpr int PH = decltype(PHtag)::value;
+    if constexpr (LV) {
+      float b[NBL];
+#pragma unroll
+      for (int j = 0; j < NBL; ++j) b[j] = rb_[j];
+      const float dti = rdti, rdt = rrdt;
+      __builtin_amdgcn_sched_barrier(0);
+      lv_load(k + 1);   // next region's rows (scalar loads in flight during this region)
+      double pd[NL], vd[NL], e1[NL], e2[NL], u[NL], a[NL], sq[NL], inc[NL];
+      f32x2 acc[NLP], x[NLP], qq[NLP], er[NLP], vl[NLP];
+      // A: f32 -> f64 desired state | basis slot 0
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { pd[d] = (double)npos[d]; vd[d] = (double)nvel[d]; }
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) acc[p] = __builtin_elementwise_fma((f32x2)b[0], tg.wp[p][0], (f32x2)0.0f);
+      __builtin_amdgcn_sched_barrier(0);
+      // B: tracking errors | basis slot 1
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { e1[d] = fsub(pd[d], v.q[d]); e2[d] = fsub(vd[d], v.qd[d]); }
+      if constexpr (NBL > 1) {
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) acc[p] = __builtin_elementwise_fma((f32x2)b[1], tg.wp[p][1], acc[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // C: gains | basis slot 2
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { e1[d] = c.pg[d] * e1[d]; e2[d] = c.dg[d] * e2[d]; }
+      if constexpr (NBL > 2) {
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) acc[p] = __builtin_elementwise_fma((f32x2)b[2], tg.wp[p][2], acc[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // D: PD sum | basis slot 3
+#pragma unroll
+      for (int d = 0; d < NL; ++d) u[d] = fadd(e1[d], e2[d]);
+      if constexpr (NBL > 3) {
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) acc[p] = __builtin_elementwise_fma((f32x2)b[3], tg.wp[p][3], acc[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // E: clip low | basis slots 4.. (NaN-free waves only: no np.clip NaN fix-up needed)
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+#ifdef FGX_EXP_NOCLIP   // timing experiment only (wrong results): no clip
+        (void)act_lo;
+#else
+        u[d] = __builtin_fmax(u[d], act_lo);
+#endif
+      }
+#pragma unroll
+      for (int j = 4; j < NBL; ++j)
+#pragma unroll
+        for (int p = 0; p < NLP; ++p) acc[p] = __builtin_elementwise_fma((f32x2)b[j], tg.wp[p][j], acc[p]);
+      __builtin_amdgcn_sched_barrier(0);
+      // F: clip high | finite difference
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+#ifdef FGX_EXP_NOCLIP
+        a[d] = u[d];
+#else
+        a[d] = __builtin_fmin(u[d], act_hi);
+#endif
+      }
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) x[p] = acc[p] - tg.cur2[p];
+      __builtin_amdgcn_sched_barrier(0);
+      // G: Euler increment, squared actions | div_rcp quotient
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { inc[d] = c.dt * a[d]; sq[d] = a[d] * a[d]; }
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) qq[p] = x[p] * rdt;
+      __builtin_amdgcn_sched_barrier(0);
+      // H: velocities, ctrl | div_rcp residual
+#pragma unroll
+      for (int d = 0; d < NL; ++d) v.qd[d] = fadd(v.qd[d], inc[d]);
+      double ctrl = fadd(sq[0], sq[1]);
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) er[p] = __builtin_elementwise_fma(-qq[p], (f32x2)dti, x[p]);
+      __builtin_amdgcn_sched_barrier(0);
+      // I: position increments, ctrl | div_rcp correction
+#pragma unroll
+      for (int d = 0; d < NL; ++d) inc[d] = c.dt * v.qd[d];
+      if constexpr (NL > 2) ctrl = fadd(ctrl, sq[2]);
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) vl[p] = __builtin_elementwise_fma(er[p], (f32x2)rdt, qq[p]);
+      __builtin_amdgcn_sched_barrier(0);
+      // J: positions, ctrl | the next sample's desired state, trajectory state
+#pragma unroll
+      for (int d = 0; d < NL; ++d) v.q[d] = fadd(v.q[d], inc[d]);
+      if constexpr (NL > 3) ctrl = fadd(ctrl, sq[3]);
+#pragma unroll
+      for (int p = 0; p < NLP; ++p) {
+        npos[2 * p] = tg.cur2[p].x;
+        nvel[2 * p] = vl[p].x;
+        if (2 * p + 1 < NL) { npos[2 * p + 1] = tg.cur2[p].y; nvel[2 * p + 1] = vl[p].y; }
+        tg.cur2[p] = acc[p];
+        tg.vprev2[p] = vl[p];
+      }
+      v.steps += 1;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int d = 4; d < NL; ++d) ctrl = fadd(ctrl, sq[d]);
+      __builtin_amdgcn_sched_barrier(0);
+      // SimpleReacher below env step 199: reward = 0 - ctrl, pushed as acc - ctrl
+      if constexpr ((PH & 4) != 0) ps.template sub_partial<J, (PH & 3)>(ctrl);
+      else ps.template sub_fast<J, PH>(ctrl);
+    }
+  };
+
   int k = 0;      // per-lane: index of the next sample
+  FGX_STAMP(o, e, 1);
   if (!LOG && ENV == ENV_SIMPLE) {   // (HoleReacher's FK + collision body is too large to unroll)
     // fast path: blocks of 8 samples with compile-time return slots and a wave-uniform sample
     // index.  Fast samples must not reach env step 199 (the only SimpleReacher step whose reward
@@ -780,7 +939,9 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     int lim = min(199, c.max_steps - 1) - v.steps;
     if (k_replan >= 0) lim = min(lim, k_replan);
     if (c.sched_state) lim = 0;   // state-dependent replanning: every sample checks the schedule
-    const int lim2 = min(Te - 1, max(0, lim));   // fast samples k < lim2 (sample Te - 1 ends the plan)
+    // fast samples k < lim2 (sample Te - 1 ends the plan; the look-ahead of the last fast sample
+    // must not be it either)
+    const int lim2 = min(Te - (MP == MP_GIVEN ? 1 : 2), max(0, lim));
     bool fast_ok = __ballot(1) == ~0ull;   // partial wave (N % 64 != 0): generic path only
     if (MP == MP_PROMP && CTRL == CTRL_PD) {
       // NaN-free waves: the PD control u = p (pos - q) + d (vel - qd) is finite for every sample
@@ -802,17 +963,33 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
     }
     const int usplit = __builtin_amdgcn_readfirstlane(split);
     if (__ballot(split != usplit) != 0) fast_ok = false;   // the block phases need one split per wave
+    // fast blocks read the basis rows with scalar loads: one plan start row per wave
+    const int s0u = __builtin_amdgcn_readfirstlane(s0);
+    if (__ballot(s0 != s0u) != 0) fast_ok = false;
+    if constexpr (MP != MP_GIVEN) tg.stab = (cfloat_ptr)(uintptr_t)s.tables + (size_t)s0u * tg.str();
     // nfast full 8-blocks, then the remainder before the first sample that needs the generic
     // path (e.g. 192..198 ahead of step 199) as one partial block of np < 8 samples
     const int lim2_min = wave_min(lim2);
     const int nfast = fast_ok ? lim2_min / 8 : 0;
     const int np = fast_ok ? lim2_min % 8 : 0;
+    if constexpr (MP != MP_GIVEN) {
+      if (nfast > 0 || np > 0) {   // look-ahead of the first fast sample
+        tg.template at<true, true>(c, 0, npos, nvel);
+        pre = true;
+        if constexpr (LV) {
+          rmax = c.rows - 1 - s0u;
+          lv_load(0);
+        }
+      }
+    }
     // Two loops: blocks before the pairwise split push into the level-1 sums a[] only, blocks from
     // the split on into the second-half sums b[] only.  (With a split, L > 128 and the result is
     // first + u: a[] and t are dead after the split, so numpy's level-1 adds there are skipped;
     // without one every block is < L <= 128 and in the first loop.)  Each loop keeps one set of 8
     // accumulators live.
-#define FGX_SAMPLE(J, PH) sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}, false);
+#define FGX_SAMPLE(J, PH)                                                                      \
+  if constexpr (LV) lv_sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}); \
+  else sample(kb + J, std::integral_constant<int, J>{}, std::integral_constant<int, PH>{}, false);
 #define FGX_BLOCK(PH) \
       FGX_SAMPLE(0, PH) FGX_SAMPLE(1, PH) FGX_SAMPLE(2, PH) FGX_SAMPLE(3, PH) \
       FGX_SAMPLE(4, PH) FGX_SAMPLE(5, PH) FGX_SAMPLE(6, PH) FGX_SAMPLE(7, PH)
@@ -841,10 +1018,12 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
 #undef FGX_BLOCK
 #undef FGX_SAMPLE
   }
+  FGX_STAMP(o, e, 2);
   while (!stop && k < Te) {
     stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG || c.sched_state);
     ++k;
   }
+  FGX_STAMP(o, e, 3);
   const int L = k;   // samples executed (trajectory_length)
   if (LOG) {
     // the full desired plan is reported (black_box_wrapper.py:245-246); the per-step arrays end
@@ -871,7 +1050,10 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   // has just computed it for its reward
   if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();
   const double ret = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
+  FGX_STAMP(o, e, 4);
   episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
+  FGX_STAMP(o, e, 5);
+  FGX_STAMP(o, e, 7);
 }
 
 // ============================================================================ step-based

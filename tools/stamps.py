@@ -1,0 +1,76 @@
+"""Per-section clocks of k_episode from the diagnostics build (-DFGX_STAMPS, _build.build_variant).
+
+  FGX_LIB=tools/ab/libfgx_stamps.so python tools/stamps.py [env_id] [envs]
+
+Lane 0 of every wave records s_memtime at: 0 kernel entry, 1 after the prologue (table staging,
+state load, trajectory init), 2 after the fast blocks, 3 after the generic samples, 4 after the
+return, 5 after the epilogue (outputs, auto-reset, state store).  Prints one JSON line with the
+median / mean cycles of each section over the waves and the spread of wave start / end times.
+"""
+import ctypes
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import fancy_gym_crowd_amd as fgx  # noqa: E402
+from fancy_gym_crowd_amd import _lib  # noqa: E402
+
+env_id = sys.argv[1] if len(sys.argv) > 1 else "fancy_ProMP/LongSimpleReacher-v0"
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+dev = torch.device("cuda", 0)
+env = fgx.make(env_id, num_envs=N, device=dev, info_level=0)
+env.reset(seed=0)
+params = torch.from_numpy(np.random.default_rng(1234).standard_normal((N, env.n_params), dtype=np.float32)).to(dev)
+obs = torch.empty((N, env.out_dim), device=dev)
+fobs = torch.empty_like(obs)
+ret = torch.empty(N, dtype=torch.float64, device=dev)
+te = torch.empty(N, dtype=torch.uint8, device=dev)
+tr = torch.empty(N, dtype=torch.uint8, device=dev)
+tl = torch.empty(N, dtype=torch.int32, device=dev)
+for _ in range(4):
+    env.step_into(params, obs, ret, te, tr, tl, fobs)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+env.step_into(params, obs, ret, te, tr, tl, fobs)
+e1.record()
+torch.cuda.synchronize()
+kern_us = e0.elapsed_time(e1) * 1e3
+lib = _lib.load()
+fn = lib.fgx_dbg_stamps
+fn.restype = ctypes.c_int
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+W = (N + 63) // 64
+buf = np.zeros(W * 8, dtype=np.uint64)
+assert fn(buf.ctypes.data, W * 8) == 0
+st = buf.reshape(W, 8)[:, :6].astype(np.int64)
+rt = buf.reshape(W, 8)[:, 6:].astype(np.int64)   # s_memrealtime (100 MHz, one clock for the GPU)
+names = ["prologue", "fast_blocks", "generic_samples", "return", "epilogue"]
+sec = np.diff(st, axis=1)
+out = {"env": env_id, "envs": N, "kernel": env.episode_kernel(), "waves": W,
+       "cycles_median": {n: int(np.median(sec[:, i])) for i, n in enumerate(names)},
+       "cycles_mean": {n: float(sec[:, i].mean()) for i, n in enumerate(names)},
+       "wave_total_median": int(np.median(st[:, 5] - st[:, 0])),
+       "kernel_us_events": kern_us}
+# s_memtime counters are per XCD (workgroup b runs on XCD b % 8): start / end spread inside each
+# XCD, and the clock rate implied by the XCD's first start to last end over the event time
+xcd = (np.arange(W) // 4) % 8
+per = []
+for x in range(8):
+    m = xcd == x
+    if m.any():
+        per.append(dict(xcd=x, start_spread=int(st[m, 0].max() - st[m, 0].min()),
+                        end_spread=int(st[m, 5].max() - st[m, 5].min()),
+                        span=int(st[m, 5].max() - st[m, 0].min())))
+out["per_xcd"] = per
+rstart, rend = rt[:, 0] - rt[:, 0].min(), rt[:, 1] - rt[:, 0].min()
+out["realtime_us"] = {"start_max": float(rstart.max() / 100), "start_median": float(np.median(rstart) / 100),
+                      "end_min": float(rend.min() / 100), "end_median": float(np.median(rend) / 100),
+                      "end_max": float(rend.max() / 100),
+                      "wave_duration_median": float(np.median(rend - rstart) / 100)}
+out["shader_ticks_per_us"] = float(np.median((st[:, 5] - st[:, 0]) / np.maximum(1, rt[:, 1] - rt[:, 0]) * 100))
+out["ticks_per_us_upper_bound"] = max(p["span"] for p in per) / kern_us
+print(json.dumps(out), flush=True)
