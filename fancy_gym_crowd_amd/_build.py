@@ -12,6 +12,7 @@ import concurrent.futures as cf
 import glob
 import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -22,7 +23,7 @@ LIB = os.path.join(HERE, "libfgx.so")
 STAMP = LIB + ".buildid"
 OBJDIR = os.path.join(HERE, "csrc", "build")
 SOURCES = ["fgx_ep_simple_gen.hip", "fgx_ep_hole_gen.hip", "fgx_ep_via_gen.hip", "fgx_ep_simple.hip",
-           "fgx_ep_hole.hip", "fgx_ep_via.hip", "fgx_api.hip"]
+           "fgx_ep_hole.hip", "fgx_ep_via.hip", "fgx_ep_jl.hip", "fgx_api.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # numerics: every expression rounds like the numpy reference; fmas only where written
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -36,7 +37,7 @@ def source_files():
 
 def source_hash():
     """16 hex digits of sha256 over the source files (name + bytes) and the compiler flags."""
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256(" ".join(FLAGS + sorted(sum(UNIT_FLAGS.values(), []))).encode())
     for f in source_files():
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -57,13 +58,56 @@ def _hipcc():
     return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+# per-unit extra flags: k_episode_jl's one-joint lanes gain nothing from SLP-pairing consecutive
+# samples (the table entries of two rows need SGPR shuffles first): plain f32 fmas
+UNIT_FLAGS = {"fgx_ep_jl.hip": ["-fno-slp-vectorize"]}
+
+
+def _deps(path, seen=None):
+    """path and the local headers it includes, transitively (#include "..." under csrc / include)."""
+    seen = set() if seen is None else seen
+    if path in seen:
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        for line in f:
+            m = re.match(r'\s*#\s*include\s+"([^"]+)"', line)
+            if m:
+                for d in (os.path.dirname(path), CSRC, INC):
+                    cand = os.path.normpath(os.path.join(d, m.group(1)))
+                    if os.path.exists(cand):
+                        _deps(cand, seen)
+                        break
+    return seen
+
+
+def _unit_key(src, bid):
+    """Object cache key of one translation unit: flags, its include closure and (fgx_api.hip only,
+    the unit that embeds it) the library build id."""
+    h = hashlib.sha256(" ".join(FLAGS + UNIT_FLAGS.get(src, [])).encode())
+    if src == "fgx_api.hip":
+        h.update(bid.encode())
+    for f in sorted(_deps(os.path.join(CSRC, src))):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _compile(src, bid, verbose):
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
-    cmd = [_hipcc(), *FLAGS, f'-DFGX_BUILD_ID="{bid}"', "-I", INC, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
+    key = _unit_key(src, bid)
+    if os.path.exists(obj) and os.path.exists(obj + ".key") and open(obj + ".key").read().strip() == key:
+        return obj   # unchanged unit: reuse its object
+    defs = [f'-DFGX_BUILD_ID="{bid}"'] if src == "fgx_api.hip" else []
+    cmd = [_hipcc(), *FLAGS, *UNIT_FLAGS.get(src, []), *defs, "-I", INC, "-c", os.path.join(CSRC, src), "-o",
+           obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(obj + ".tmp", obj)
+    with open(obj + ".key", "w") as f:
+        f.write(key)
     return obj
 
 
@@ -76,11 +120,16 @@ def build_variant(out, defines=(), verbose=False):
 
     def one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [_hipcc(), *FLAGS, *[f"-D{d}" for d in defines], f'-DFGX_BUILD_ID="{bid}"', "-I", INC, "-c",
-               os.path.join(CSRC, src), "-o", obj]
+        key = _unit_key(src, bid) + ",".join(defines)
+        if os.path.exists(obj) and os.path.exists(obj + ".key") and open(obj + ".key").read().strip() == key:
+            return obj
+        cmd = [_hipcc(), *FLAGS, *UNIT_FLAGS.get(src, []), *[f"-D{d}" for d in defines], f'-DFGX_BUILD_ID="{bid}"',
+               "-I", INC, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+        with open(obj + ".key", "w") as f:
+            f.write(key)
         return obj
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(one, SOURCES))

@@ -19,6 +19,9 @@ FGX_DECLARE_LAUNCH(fgx_launch_episode_simple_gen)
 FGX_DECLARE_LAUNCH(fgx_launch_episode_hole_gen)
 FGX_DECLARE_LAUNCH(fgx_launch_episode_via_gen)
 #undef FGX_DECLARE_LAUNCH
+// k_episode_jl instantiations (fgx_ep_jl.hip): nbs = the compiled basis count (5, or 0 = generic)
+int fgx_launch_episode_jl(const fgx::DevCfg& c, const fgx::DevState& s, int mp, int nbs, const float* params,
+                          const fgx::Outputs& o, hipStream_t stream, std::string& err);
 
 namespace fgx {
 
@@ -36,7 +39,7 @@ namespace fgx {
 //    DMP at every size (up to 2.7x).  Short replanning segments pay its per-chunk exchange.
 //  * k_episode_ws wins for 2-link ProDMP up to one full round (~10%, also with replanning).
 // FGX_EPISODE_KERNEL=classic|jp|ws forces a kernel wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2 };
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -58,6 +61,7 @@ inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env
     if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
     if (std::strcmp(v, "jp") == 0) return EK_JP;
     if (std::strcmp(v, "ws") == 0) return EK_WS;
+    if (std::strcmp(v, "jl") == 0) return EK_JL;
   }
   const int64_t R = round_envs(), tail = c.N % R;
   if (c.nl == 5) {
@@ -132,6 +136,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
+    if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
   }
   if (log)
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), lds, stream, c, s,

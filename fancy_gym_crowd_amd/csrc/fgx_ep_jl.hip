@@ -1,0 +1,54 @@
+// k_episode_jl instantiations (fgx_jl.h): SimpleReacher + PD, every MP kind, 2 / 5 links, the
+// registered basis count (NB = 5) and the generic one (NB = 0).  A translation unit of its own so
+// that the build compiles it in parallel with the k_episode units.
+#include "fgx_dispatch.h"
+#include "fgx_jl.h"
+
+namespace {
+template <int MP, int NL, int NB>
+int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
+              hipStream_t stream, std::string& err) {
+  using S = fgx::JlShape<NL>;
+  if constexpr (NB != 0) {
+    if (c.stride != fgx::Traj<MP, 1, NB>::KS) {
+      err = "basis table stride does not match the compiled layout";
+      return -1;
+    }
+  }
+  const unsigned blocks = (unsigned)((c.N + S::EPB - 1) / S::EPB);
+  hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB>), dim3(blocks), dim3(64 * S::WAVES), S::lds_bytes(), stream, c,
+                     s, params, o);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { err = std::string("k_episode_jl launch: ") + hipGetErrorString(e); return -2; }
+  return 0;
+}
+
+template <int MP, int NB>
+int launch_jl_nl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
+                 hipStream_t stream, std::string& err) {
+  if (c.nl == 2) return launch_jl<MP, 2, NB>(c, s, params, o, stream, err);
+  if (c.nl == 5) return launch_jl<MP, 5, NB>(c, s, params, o, stream, err);
+  err = "k_episode_jl: n_links not instantiated (supported: 2, 5)";
+  return -4;
+}
+
+template <int NB>
+int launch_jl_mp(const fgx::DevCfg& c, const fgx::DevState& s, int mp, const float* params, const fgx::Outputs& o,
+                 hipStream_t stream, std::string& err) {
+  switch (mp) {
+    case fgx::MP_PROMP: return launch_jl_nl<fgx::MP_PROMP, NB>(c, s, params, o, stream, err);
+    case fgx::MP_DMP: return launch_jl_nl<fgx::MP_DMP, NB>(c, s, params, o, stream, err);
+    case fgx::MP_PRODMP: return launch_jl_nl<fgx::MP_PRODMP, NB>(c, s, params, o, stream, err);
+  }
+  err = "k_episode_jl: bad mp kind";
+  return -1;
+}
+}  // namespace
+
+int fgx_launch_episode_jl(const fgx::DevCfg& c, const fgx::DevState& s, int mp, int nbs, const float* params,
+                          const fgx::Outputs& o, hipStream_t stream, std::string& err) {
+  if (nbs == 5) return launch_jl_mp<5>(c, s, mp, params, o, stream, err);
+  if (nbs == 0) return launch_jl_mp<0>(c, s, mp, params, o, stream, err);
+  err = "k_episode_jl: basis count not instantiated";
+  return -4;
+}

@@ -604,13 +604,14 @@ __device__ inline bool state_replan(const DevCfg& c, const Env<NL>& v) {
 // the env after its last sample with FK refreshed.
 template <int NL>
 __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState& s, const Outputs& o, int64_t e,
-                                                 Env<NL>& v, int plans, int L, double ret, bool term, bool trunc) {
+                                                 Env<NL>& v, int plans, int L, double ret, bool term, bool trunc,
+                                                 bool count = true) {
   const int64_t N = c.N;
   o.ret[e] = ret;
   o.term[e] = term;
   o.trunc[e] = trunc;
   o.tlen[e] = L;
-  if (o.inner_steps) {   // wave-reduce the trajectory lengths, one atomic per (full) wave
+  if (count && o.inner_steps) {   // (count = false: the caller adds L to inner_steps itself)   // wave-reduce the trajectory lengths, one atomic per (full) wave
     if (__ballot(1) == ~0ull) {
       long long sum = L;
 #pragma unroll

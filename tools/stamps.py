@@ -1,6 +1,9 @@
 """Per-section clocks of k_episode from the diagnostics build (-DFGX_STAMPS, _build.build_variant).
 
-  FGX_LIB=tools/ab/libfgx_stamps.so python tools/stamps.py [env_id] [envs]
+  FGX_LIB=tools/ab/libfgx_stamps.so [FGX_EPISODE_KERNEL=jl] python tools/stamps.py [env_id] [envs]
+
+k_episode_jl: 0 entry, 1 after the prologue, 2 after the fast chunk pipeline, 3 after the generic
+chunks, 4 after the gather barriers, 5 after the return and epilogue (wave 0 of each workgroup).
 
 Lane 0 of every wave records s_memtime at: 0 kernel entry, 1 after the prologue (table staging,
 state load, trajectory init), 2 after the fast blocks, 3 after the generic samples, 4 after the
@@ -43,18 +46,26 @@ lib = _lib.load()
 fn = lib.fgx_dbg_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-W = (N + 63) // 64
+kern = env.episode_kernel()
+if kern == "k_episode_jl":
+    epb = 4 * (64 // env._eng.cfg.n_links)
+    W = (N + epb - 1) // epb * 4
+else:
+    W = (N + 63) // 64
 buf = np.zeros(W * 8, dtype=np.uint64)
 assert fn(buf.ctypes.data, W * 8) == 0
 st = buf.reshape(W, 8)[:, :6].astype(np.int64)
 rt = buf.reshape(W, 8)[:, 6:].astype(np.int64)   # s_memrealtime (100 MHz, one clock for the GPU)
-names = ["prologue", "fast_blocks", "generic_samples", "return", "epilogue"]
+names = (["prologue", "fast_chunks", "slow_chunks", "gather", "return_epilogue"] if kern == "k_episode_jl" else
+         ["prologue", "fast_blocks", "generic_samples", "return", "epilogue"])
 sec = np.diff(st, axis=1)
 out = {"env": env_id, "envs": N, "kernel": env.episode_kernel(), "waves": W,
        "cycles_median": {n: int(np.median(sec[:, i])) for i, n in enumerate(names)},
        "cycles_mean": {n: float(sec[:, i].mean()) for i, n in enumerate(names)},
        "wave_total_median": int(np.median(st[:, 5] - st[:, 0])),
        "kernel_us_events": kern_us}
+if kern == "k_episode_jl":   # the epilogue runs in wave 0 of each workgroup
+    out["cycles_median_wave0"] = {n: int(np.median(sec[::4, i])) for i, n in enumerate(names)}
 # s_memtime counters are per XCD (workgroup b runs on XCD b % 8): start / end spread inside each
 # XCD, and the clock rate implied by the XCD's first start to last end over the event time
 xcd = (np.arange(W) // 4) % 8
