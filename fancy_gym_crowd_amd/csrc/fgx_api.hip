@@ -318,6 +318,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_seed = off; off = align_up(off + sizeof(uint64_t) * N);
   const size_t o_start = off; off = align_up(off + sizeof(double) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
+  const size_t o_tabt = off; off = align_up(off + sizeof(float) * (size_t)tables_t_rows(h->dc.rows) * h->dc.stride);
   // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128)
   const bool need_rew = (cfg->env_kind != FGX_ENV_SIMPLE || h->dc.sched_state) && cfg->mp_kind != FGX_MP_NONE &&
                         h->dc.T > 128;
@@ -339,6 +340,7 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.rew = need_rew ? (double*)(b + o_rew) : nullptr;
   h->st.plan_len = nullptr;
   h->st.tables = h->tables;
+  h->st.tables_t = (const float*)(b + o_tabt);
   h->st.start = (double*)(b + o_start);
   (void)hipMemset(h->state_block, 0, off);
   if (h->learned()) {
@@ -367,6 +369,11 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
     if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_NOMEM, "hipMalloc scratch"); }
     hipLaunchKernelGGL(k_tables_prodmp, dim3(1), dim3(256), 0, 0, d, cfg->tau, cfg->alpha_phase, cfg->bandwidth,
                        h->scratch, h->tables);
+  }
+  if (d.mp != MP_NONE && d.rows > 0) {
+    const int n = tables_t_rows(d.rows) * d.stride;
+    hipLaunchKernelGGL(k_tables_transpose, dim3((n + 255) / 256), dim3(256), 0, 0, d.rows, d.stride, d.nb, h->tables,
+                       (float*)(b + o_tabt));
   }
   e = hipGetLastError();
   if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("table kernel: ") + hipGetErrorString(e)); }

@@ -83,7 +83,16 @@ struct DevState {
                    //        the exact numpy pairwise return for lengths 128 < L <= T
   const int32_t* plan_len;   // [N] per-env plan length (learned tau / sub-trajectories) or null
   const float* tables;
+  // the same table column-major, [stride][tables_t_rows(rows)]: column j, row r at
+  // j * RT + r + tables_t_pad(j, nb) (k_episode_jl's ProMP chunks load 8 consecutive rows of one
+  // column with one 32-byte-aligned scalar load)
+  const float* tables_t;
 };
+
+__host__ __device__ inline int tables_t_rows(int rows) { return (rows + 32 + 7) & ~7; }
+// basis columns start their rows at offset 6 (a chunk reads rows k0 + 2 ..), the dt columns at 7
+// (rows k0 + 1 ..): both land on multiples of 8 for k0 % 8 == 0
+__host__ __device__ inline int tables_t_pad(int col, int nb) { return col < nb ? 6 : 7; }
 
 struct Outputs {
   float* obs;        // [N, out_dim]
@@ -325,6 +334,20 @@ struct Env {
       c[k] = cs; s[k] = sn;
       x = (k == 0) ? cs : x + cs;
       y = (k == 0) ? sn : y + sn;
+      jx[k + 1] = 0.0 + x;
+      jy[k + 1] = 0.0 + y;
+    }
+  }
+  // the same FK given cos / sin of the cumulative angles (computed elsewhere with the same sincos of
+  // the same angles, e.g. one joint per lane in k_episode_jl)
+  __device__ __forceinline__ void fk_given(const double* cs, const double* sn) {
+    double x = 0.0, y = 0.0;
+    jx[0] = 0.0; jy[0] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      c[k] = cs[k]; s[k] = sn[k];
+      x = (k == 0) ? cs[k] : x + cs[k];
+      y = (k == 0) ? sn[k] : y + sn[k];
       jx[k + 1] = 0.0 + x;
       jy[k + 1] = 0.0 + y;
     }

@@ -4,6 +4,9 @@
 #include "fgx_dispatch.h"
 #include "fgx_jl.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 template <int MP, int NL, int NB>
 int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
@@ -15,9 +18,12 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
       return -1;
     }
   }
-  const unsigned blocks = (unsigned)((c.N + S::EPB - 1) / S::EPB);
+  int gw = S::G;   // (fewer envs per wave measured slower at every N: profiles/r02_jl_scan.jsonl)
+  if (const char* v = std::getenv("FGX_JL_GW")) gw = std::max(1, std::min(S::G, std::atoi(v)));   // experiments
+  const int64_t per_block = (int64_t)S::WAVES * gw;
+  const unsigned blocks = (unsigned)((c.N + per_block - 1) / per_block);
   hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB>), dim3(blocks), dim3(64 * S::WAVES), S::lds_bytes(), stream, c,
-                     s, params, o);
+                     s, params, o, gw);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { err = std::string("k_episode_jl launch: ") + hipGetErrorString(e); return -2; }
   return 0;

@@ -34,12 +34,24 @@
 namespace fgx {
 
 template <int NL>
+struct JlShape;
+
+// envs per wave for N envs on `simds` SIMDs: the most (64 / NL) once N fills every SIMD, fewer below,
+// so that a small shard still puts one wave on every SIMD instead of two waves on some
+inline int jl_envs_per_wave(int64_t N, int64_t simds, int G) {
+  const int64_t g = (N + simds - 1) / simds;
+  return (int)(g < 1 ? 1 : (g > G ? G : g));
+}
+
+template <int NL>
 struct JlShape {
   static constexpr int G = 64 / NL;             // envs per wave
   static constexpr int WAVES = 4;               // waves per workgroup
   static constexpr int EPB = G * WAVES;         // envs per workgroup
   static constexpr int SPW = (8 + NL - 1) / NL; // pairwise slots owned per lane
-  static constexpr int GF = 25 + 2 * NL;        // gathered f64 per env: A, B, tail (8 each), cfk, q, qd
+  // gathered f64 per env: A, B, tail (8 each), cfk, q, qd, then cos / sin of the cumulative angles
+  // (FK) and of every q (observation)
+  static constexpr int GF = 25 + 6 * NL;
   static constexpr size_t lds_bytes() {
     const size_t ex = (size_t)WAVES * 16 * 64 * sizeof(double);
     const size_t ga = (size_t)GF * EPB * sizeof(double);
@@ -56,18 +68,22 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 template <int MP, int NL, int NB>
-__global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const float* __restrict__ params, Outputs o) {
+// gw: envs per wave actually used (<= G; fewer than G spreads a small N over more SIMDs, see
+// jl_envs_per_wave); LDS slots keep the compile-time stride G
+__global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const float* __restrict__ params, Outputs o,
+                                                    int gw) {
   using S = JlShape<NL>;
   constexpr int G = S::G, EPB = S::EPB, SPW = S::SPW;
+  constexpr int NBL = NB > 0 ? NB : 1;
   extern __shared__ double lds_jl[];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   double* ex = lds_jl + w * (16 * 64);  // this wave's two chunk buffers: a^2 of sample j at [j * 64 + lane]
   const int g = lane / NL, d = lane - g * NL;
   const int64_t N = c.N;
-  const int slot = w * G + g;           // env of this lane within the workgroup
-  const int64_t e0 = (int64_t)blockIdx.x * EPB + slot;
-  const bool valid = g < G && e0 < N;
+  const int slot = w * G + g;           // LDS slot of this lane's env
+  const int64_t e0 = (int64_t)blockIdx.x * (S::WAVES * gw) + w * gw + g;
+  const bool valid = g < gw && e0 < N;
   const int64_t e = valid ? e0 : N - 1;   // clamped: loads stay in bounds, nothing is stored
   const uint64_t vmask = __ballot(valid);
   const int64_t wst = ((int64_t)blockIdx.x * S::WAVES + w) * 64;   // diagnostics build: stamp slot of this wave
@@ -128,8 +144,9 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     }
   };
   // the joint's PD -> clip -> torque Euler recurrence over chunk k0 (black_box_wrapper.py:201-205,
-  // base_reacher_torque.py:20-37): sq[j] = a^2.  FAST: every valid lane runs all 8 samples.  EXACT:
-  // np.clip's NaN propagation; otherwise a NaN u is recorded in nanm (the chunk is then re-run)
+  // base_reacher_torque.py:20-37): sq[j] = a^2.  FAST: every valid lane runs all 8 samples.  EXACT
+  // 1: np.clip's NaN propagation; 0: a NaN u is recorded in nanm (the segment is then re-run);
+  // 2: the wave is NaN-free (proven), neither
   auto dyn = [&](int k0, const float* P, const float* V, double* sq, auto fast, auto exact)
       __attribute__((always_inline)) {
 #pragma unroll
@@ -137,9 +154,9 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
       sq[j] = 0.0;
       if (decltype(fast)::value || k0 + j < sg.L) {
         const double u = fadd(pg * fsub((double)P[j], q), dg * fsub((double)V[j], qd));
-        double a = clip_nonan(u, act_lo, act_hi);
-        if constexpr (decltype(exact)::value) a = (u != u) ? u : a;
-        else nanm |= __ballot(u != u);
+        double a = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);   // v_max / v_min: a NaN u gives a bound
+        if constexpr (decltype(exact)::value == 1) a = (u != u) ? u : a;
+        else if constexpr (decltype(exact)::value == 0) nanm |= __ballot(u != u);
         qd = fadd(qd, dt * a);
         q = fadd(q, dt * qd);
         sq[j] = a * a;
@@ -201,43 +218,137 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
 
   // Fast chunk pipeline (waves whose valid lanes share one segment layout and plan start row): one
   // branch-free basic block per chunk that evaluates chunk ch + 1's trajectory (independent f32
-  // work, basis rows by scalar loads at constant offsets from one chunk base), runs chunk ch's f64
-  // recurrence, reduces chunk ch - 1 into one pairwise phase fixed at compile time (PH 1: the
-  // first-half slots A, PH 2: the second-half slots B) and writes chunk ch's rows.  A lone wave
-  // per SIMD (shard sizes) issues every instruction, SALU and selects included, at ~6 cycles:
-  // nothing here is per-lane control flow.
+  // work, basis rows by scalar loads), runs chunk ch's f64 recurrence, reduces chunk ch - 1 into
+  // one pairwise phase fixed at compile time (PH 1: the first-half slots A, PH 2: the second-half
+  // slots B) and writes chunk ch's rows.  A lone wave per SIMD (shard sizes) issues every
+  // instruction, SALU and selects included, at ~6 cycles: nothing here is per-lane control flow.
+  //
+  // ProMP (PKT): the chunk's trajectory comes from the column-major table (DevState::tables_t):
+  // one 8-row scalar load per basis column and per dt column, the 8 look-ahead positions as 4
+  // pairs of samples (v_pk_fma_f32 over two table rows, the same k-ordered fma chain per sample),
+  // the forward differences and div_rcp on the same pairs: bit-identical to Traj::at.  Chunks past
+  // the plan's end read rows inside the padded table and are never run; the plan's last sample
+  // (vel = the previous velocity, Traj::at's k == T - 1 branch) is patched once, in a peeled
+  // iteration.  ProMP waves take the fast path only when NaN-free (the k_episode guard), so the
+  // fast recurrence records no NaN controls.
+  constexpr bool PKT = (MP == MP_PROMP) && NB > 0;
+  typedef float f8u __attribute__((ext_vector_type(8), aligned(4)));
+  typedef const f8u __attribute__((address_space(4)))* cf8_ptr;
   float plast = 0.0f, vlast = 0.0f;   // desired state of the last fast sample
-  auto traj_fast = [&](int k0, float* Pt, float* Vt) __attribute__((always_inline)) {
-    const cfloat_ptr base = tg.stab + (size_t)k0 * tg.str();
+  // ProMP chunk columns: basis columns j (rows R + 2 ..), dt and 1/dt (rows R + 1 ..) of chunk k0
+  struct Cols { f8u b[NBL]; f8u dt, rd; };
+  auto traj_load = [&](int k0, Cols& cl) __attribute__((always_inline)) {
+    if constexpr (PKT) {
+      const int RT = tables_t_rows(c.rows);
+      const int R = s0u + k0;   // absolute row of sample k0: its dt row is R + 1, its next basis row R + 2
+      const cfloat_ptr tt = (cfloat_ptr)(uintptr_t)s.tables_t;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float p1[1], v1[1];
-      tg.template at_rows<true>(c, k0 + j, base + (j + 1) * tg.str(), p1, v1);
-      Pt[j] = p1[0];
-      Vt[j] = v1[0];
+      for (int j = 0; j < NBL; ++j) cl.b[j] = *(cf8_ptr)(tt + (size_t)j * RT + R + 8);
+      cl.dt = *(cf8_ptr)(tt + (size_t)NBL * RT + R + 8);
+      cl.rd = *(cf8_ptr)(tt + (size_t)(NBL + 1) * RT + R + 8);
     }
   };
-  auto reduce_fast = [&](int ch, auto ph) __attribute__((always_inline)) {
+  auto traj_fast = [&](int k0, const Cols& cl, float* Pt, float* Vt) __attribute__((always_inline)) {
+    if constexpr (PKT) {
+      // sample pairs (2i, 2i + 1): rows (R + 2 + 2i, R + 3 + 2i) of basis column j, and the dt / 1/dt
+      // entries of rows (R + 1 + 2i, R + 2 + 2i)
+      f32x2 acc[4] = {};
+#pragma unroll
+      for (int j = 0; j < NBL; ++j) {
+        const f8u col = cl.b[j];
+        const f32x2 wj = (f32x2)tg.w[0][j];
+        acc[0] = __builtin_elementwise_fma(__builtin_shufflevector(col, col, 0, 1), wj, acc[0]);
+        acc[1] = __builtin_elementwise_fma(__builtin_shufflevector(col, col, 2, 3), wj, acc[1]);
+        acc[2] = __builtin_elementwise_fma(__builtin_shufflevector(col, col, 4, 5), wj, acc[2]);
+        acc[3] = __builtin_elementwise_fma(__builtin_shufflevector(col, col, 6, 7), wj, acc[3]);
+      }
+      const f8u dt8 = cl.dt, rd8 = cl.rd;
+      const f32x2 rdp[4] = {__builtin_shufflevector(rd8, rd8, 0, 1), __builtin_shufflevector(rd8, rd8, 2, 3),
+                            __builtin_shufflevector(rd8, rd8, 4, 5), __builtin_shufflevector(rd8, rd8, 6, 7)};
+      const f32x2 dtp[4] = {__builtin_shufflevector(dt8, dt8, 0, 1), __builtin_shufflevector(dt8, dt8, 2, 3),
+                            __builtin_shufflevector(dt8, dt8, 4, 5), __builtin_shufflevector(dt8, dt8, 6, 7)};
+      float cr[9];
+      cr[0] = tg.cur[0];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cr[2 * i + 1] = acc[i].x;
+        cr[2 * i + 2] = acc[i].y;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x2 x = {cr[2 * i + 1] - cr[2 * i], cr[2 * i + 2] - cr[2 * i + 1]};
+        const f32x2 rd = rdp[i], dd = dtp[i];
+        const f32x2 qv = x * rd;                                     // div_rcp on the pair
+        const f32x2 er = __builtin_elementwise_fma(-qv, dd, x);
+        const f32x2 vl = __builtin_elementwise_fma(er, rd, qv);
+        Pt[2 * i] = cr[2 * i];
+        Pt[2 * i + 1] = cr[2 * i + 1];
+        Vt[2 * i] = vl.x;
+        Vt[2 * i + 1] = vl.y;
+      }
+      tg.cur[0] = cr[8];
+      tg.vprev[0] = Vt[7];
+    } else {
+      (void)cl;
+      const cfloat_ptr base = tg.stab + (size_t)k0 * tg.str();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p1[1], v1[1];
+        tg.template at_rows<true>(c, k0 + j, base + (j + 1) * tg.str(), p1, v1);
+        Pt[j] = p1[0];
+        Vt[j] = v1[0];
+      }
+    }
+  };
+  auto reduce_load = [&](int ch, double (*rv)[NL]) __attribute__((always_inline)) {
     const double* b = ex + (ch & 1) * 512;
 #pragma unroll
     for (int sl = 0; sl < SPW; ++sl) {
       const int j = d + NL * sl;
       const int jj = j < 8 ? j : 0;   // (lanes without this slot accumulate a discarded sum)
       const double* row = b + jj * 64 + gr * NL;
-      double ctrl = row[0];
 #pragma unroll
-      for (int dd = 1; dd < NL; ++dd) ctrl = fadd(ctrl, row[dd]);
+      for (int dd = 0; dd < NL; ++dd) rv[sl][dd] = row[dd];
+    }
+  };
+  auto reduce_fast = [&](double (*rv)[NL], auto ph) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sl = 0; sl < SPW; ++sl) {
+      double ctrl = rv[sl][0];
+#pragma unroll
+      for (int dd = 1; dd < NL; ++dd) ctrl = fadd(ctrl, rv[sl][dd]);
       const double r = 0.0 - ctrl;
       if constexpr (decltype(ph)::value == 1) A[sl] = fadd(A[sl], r);
       else B[sl] = fadd(B[sl], r);
     }
   };
-  auto fast_iter = [&](int ch, const float* Pc, const float* Vc, float* Pt, float* Vt, auto ph)
-      __attribute__((always_inline)) {
+  // the chunk holding the plan's last sample T - 1 (computed as a look-ahead like any other chunk)
+  // gets Traj::at's k == T - 1 velocity (the previous one) before it runs: a uniform branch at the
+  // top of the iteration, outside the chunk's basic block
+  const int cpch = (c.T - 1) / 8, ip = (c.T - 1) & 7;
+  auto fast_iter = [&](int ch, float* Pc, float* Vc, float* Pt, float* Vt, auto ph) __attribute__((always_inline)) {
     const int k0 = ch * 8;
-    traj_fast(k0 + 8, Pt, Vt);
-    dyn(k0, Pc, Vc, sq, std::true_type{}, std::false_type{});
-    if constexpr (decltype(ph)::value != 0) reduce_fast(ch - 1, ph);
+    if constexpr (PKT) {
+      if (__builtin_expect(ch == cpch, 0)) {
+        float prev = vlast;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float vj = Vc[j];
+          if (j == ip) Vc[j] = prev;
+          prev = vj;
+        }
+      }
+    }
+    // issue the chunk's memory reads first (scalar column loads, the previous chunk's LDS rows): their
+    // latency runs under the f64 recurrence
+    Cols cl;
+    traj_load(k0 + 8, cl);
+    double rv[SPW][NL];
+    if constexpr (decltype(ph)::value != 0) reduce_load(ch - 1, rv);
+    __builtin_amdgcn_sched_barrier(0);
+    traj_fast(k0 + 8, cl, Pt, Vt);
+    dyn(k0, Pc, Vc, sq, std::true_type{}, std::integral_constant<int, PKT ? 2 : 0>{});   // ProMP: NaN-free
+    if constexpr (decltype(ph)::value != 0) reduce_fast(rv, ph);
     write_sq(ch, sq);
     wave_lds_sync();
     plast = Pc[7];
@@ -257,6 +368,17 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
       for (int j = 0; j < 8; ++j) { P[j] = Pn[j]; V[j] = Vn[j]; }
     }
   };
+  // ProMP NaN-free waves (k_episode's guard): with |w| < 1e30 and |q|, |qd|, |p|, |d| < 1e150 every
+  // PD control u of the plan is finite, so np.clip's NaN propagation never applies
+  bool nan_free = true;
+  if constexpr (PKT) {
+    bool ok = __builtin_fabs(c.act_lo) <= 1e3 && __builtin_fabs(c.act_hi) <= 1e3 && c.dt <= 1.0 &&
+              __builtin_fabs(q) < 1e150 && __builtin_fabs(qd) < 1e150 && __builtin_fabs(pg) < 1e150 &&
+              __builtin_fabs(dg) < 1e150;
+#pragma unroll
+    for (int j = 0; j < NBL; ++j) ok = ok && __builtin_fabsf(tg.w[0][j]) < 1e30f;
+    nan_free = __ballot(valid && !ok) == 0;
+  }
 
   // EXACT = false records NaN controls in nanm instead of propagating them; the caller then re-runs
   // the whole segment with EXACT = true on the generic loop.
@@ -265,18 +387,19 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (nchunks == 0) return;
     traj(0, P, V, std::false_type{}, sc);
     int ch = 0;
-    if constexpr (decltype(sc)::value && !decltype(exact)::value) {
+    if constexpr (decltype(sc)::value && decltype(exact)::value == 0) {
       if (Lmin == Lmax) {   // one segment layout for the wave: uniform phases
         const int L = Lmin;
         const int hs = __builtin_amdgcn_readlane(sg.hs, lead), bend = __builtin_amdgcn_readlane(sg.bend, lead);
         const int kfk = __builtin_amdgcn_readlane(sg.k_fk, lead);
-        // fast iteration ch: chunk ch runs on every lane (8 ch + 8 <= L), chunk ch + 1's samples
-        // are below T - 1 (8 ch + 16 < T), and chunk ch - 1 lies before the tail and the FK sample
-        // (8 ch <= bend, 8 ch <= kfk)
-        int nf = min(L / 8, (c.T - 16 + 7) / 8);
-        nf = min(nf, bend / 8 + 1);
+        // fast iteration ch: chunk ch runs on every lane (8 ch + 8 <= L), chunk ch - 1 lies before
+        // the tail and the FK sample (8 ch <= bend, 8 ch <= kfk) and, generic trajectories only,
+        // chunk ch + 1's samples are below T - 1 (8 ch + 16 < T)
+        int nf = min(L / 8, bend / 8 + 1);
+        if (!PKT) nf = min(nf, (c.T - 16 + 7) / 8);
         if (kfk < 0x7fffffff) nf = min(nf, kfk / 8 + 1);
         nf = max(0, min(nf, nchunks));
+        if (!nan_free) nf = 0;
         if (nf > 0) {
           fast_range(0, 1, std::integral_constant<int, 0>{});
           const int na = min(nf, hs / 8 + 1);   // iterations reducing first-half chunks
@@ -302,13 +425,13 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   };
   nanm = 0;
   FGX_STAMP(o, wst, 1);
-  if (s0_uni) run(std::true_type{}, std::false_type{});
-  else run(std::false_type{}, std::false_type{});
+  if (s0_uni) run(std::true_type{}, std::integral_constant<int, 0>{});
+  else run(std::false_type{}, std::integral_constant<int, 0>{});
   if (__builtin_expect((nanm & vmask) != 0, 0)) {   // a NaN control: np.clip semantics from the start
     wave_lds_sync();
     restart();
-    if (s0_uni) run(std::true_type{}, std::true_type{});
-    else run(std::false_type{}, std::true_type{});
+    if (s0_uni) run(std::true_type{}, std::integral_constant<int, 1>{});
+    else run(std::false_type{}, std::integral_constant<int, 1>{});
   }
 
   if (valid && sg.stop && c.cond_desired) {   // black_box_wrapper.py:234-236
@@ -335,11 +458,30 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     ga[(25 + NL + d) * EPB + slot] = qd;
   }
   __syncthreads();
+  // the epilogue's trigonometry, one joint per lane: cos / sin of the cumulative angle q0 + ... + qd
+  // (numpy cumsum order, Env::fk) and of qd itself (the observation, emit_obs)
+  if (g < G) {
+    double ang = ga[25 * EPB + slot];
+#pragma unroll
+    for (int k = 1; k < NL; ++k) {
+      const double nx = ang + ga[(25 + k) * EPB + slot];
+      ang = (k <= d) ? nx : ang;
+    }
+    double fs, fc, os_, oc;
+    sincos(ang, &fs, &fc);
+    sincos(q, &os_, &oc);
+    ga[(25 + 2 * NL + d) * EPB + slot] = fc;
+    ga[(25 + 3 * NL + d) * EPB + slot] = fs;
+    ga[(25 + 4 * NL + d) * EPB + slot] = oc;
+    ga[(25 + 5 * NL + d) * EPB + slot] = os_;
+  }
+  __syncthreads();
 
   // ---- one thread per env: return and epilogue
   const int t = threadIdx.x;
-  const int64_t et = (int64_t)blockIdx.x * EPB + t;
-  const bool tv = t < EPB && et < N;
+  const int tw = t / G, tg_ = t - tw * G;   // slot t = tw * G + tg_
+  const int64_t et = (int64_t)blockIdx.x * (S::WAVES * gw) + tw * gw + tg_;
+  const bool tv = t < EPB && tg_ < gw && et < N;
   if (o.inner_steps) {   // sum of trajectory lengths: one atomic per wave
     JpSeg st;
     st.init(c, s, tv ? et : N - 1, tv);
@@ -362,7 +504,15 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   for (int k = 0; k < NL; ++k) { v.q[k] = ga[(25 + k) * EPB + t]; v.qd[k] = ga[(25 + NL + k) * EPB + t]; }
   v.steps = st.steps + st.L;
   if (st.stop && c.cond_desired) v.flags |= 2u;
-  v.fk();
+  double fc[NL], fs[NL], oc[NL], os_[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    fc[k] = ga[(25 + 2 * NL + k) * EPB + t];
+    fs[k] = ga[(25 + 3 * NL + k) * EPB + t];
+    oc[k] = ga[(25 + 4 * NL + k) * EPB + t];
+    os_[k] = ga[(25 + 5 * NL + k) * EPB + t];
+  }
+  v.fk_given(fc, fs);
   // the last sample at env step 199 (simple_reacher.py:60-62): r = -dist(ee, goal) - sum a^2; it is
   // the last element of the return sum, either the sequential tail's last or slot 7 of the last
   // 8-block (L == bend)
@@ -380,7 +530,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (j < ntail) res = res + ((fk_last && j == ntail - 1) ? r_fk : ga[(3 * j + 2) * EPB + t]);
   if (L > 128) res = PairwiseSum::comb(sa) + res;
   const bool trunc = v.steps >= c.max_steps;
-  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false);
+  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_);
   FGX_STAMP(o, wst, 5);
   FGX_STAMP(o, wst, 7);
 }

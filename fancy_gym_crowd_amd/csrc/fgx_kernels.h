@@ -25,9 +25,11 @@ namespace fgx {
 // fresh: v was just reset (Env::reset): q = [q0, +0, ..., +0] and fk() has run, so cos / sin of
 // q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
 // fk0: FK is current for q (k_episode's epilogue), so cos / sin of q[0] are c[0] / s[0].
+// gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
-                                         bool fresh = false, bool fk0 = false) {
+                                         bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
+                                         const double* gsn = nullptr) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
@@ -45,7 +47,8 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
     } else {
 #pragma unroll
       for (int k = 0; k < NL; ++k) {
-        if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
+        if (gcs) { cs[k] = gcs[k]; sn[k] = gsn[k]; }
+        else if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
         else sincos(v.q[k], &sn[k], &cs[k]);
       }
     }
@@ -605,7 +608,8 @@ __device__ inline bool state_replan(const DevCfg& c, const Env<NL>& v) {
 template <int NL>
 __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState& s, const Outputs& o, int64_t e,
                                                  Env<NL>& v, int plans, int L, double ret, bool term, bool trunc,
-                                                 bool count = true) {
+                                                 bool count = true, const double* gcs = nullptr,
+                                                 const double* gsn = nullptr) {
   const int64_t N = c.N;
   o.ret[e] = ret;
   o.term[e] = term;
@@ -624,13 +628,13 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   float* ob = o.obs + e * c.out_dim;
   float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
   if (o.autoreset && (term || trunc)) {
-    if (fo) emit_obs(c, v, c.return_context, fo, nullptr, false, true);
+    if (fo) emit_obs(c, v, c.return_context, fo, nullptr, false, true, gcs, gsn);
     autoreset_env(c, s, e, v);
     plans = 0;
     v.flags = 0;
     emit_obs(c, v, c.return_context, ob, nullptr, true);
   } else {
-    emit_obs(c, v, c.return_context, ob, fo, false, true);
+    emit_obs(c, v, c.return_context, ob, fo, false, true, gcs, gsn);
   }
   store_env(c, s, e, v, c.env != ENV_SIMPLE);
   s.plans[e] = plans;

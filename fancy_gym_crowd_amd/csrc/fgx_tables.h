@@ -158,4 +158,13 @@ __global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw,
     prodmp_row(c, (double)i * h, dp + (size_t)i * W, dp + (size_t)i * W + nb, tab + (size_t)i * c.stride);
 }
 
+// column-major copy of the shared table (DevState::tables_t)
+__global__ void k_tables_transpose(int rows, int stride, int nb, const float* tab, float* tt) {
+  const int RT = tables_t_rows(rows);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= stride * RT) return;
+  const int col = i / RT, r = i - col * RT - tables_t_pad(col, nb);
+  tt[i] = (r >= 0 && r < rows) ? tab[(size_t)r * stride + col] : 0.0f;
+}
+
 }  // namespace fgx

@@ -64,6 +64,13 @@ out = {"env": env_id, "envs": N, "kernel": env.episode_kernel(), "waves": W,
        "cycles_mean": {n: float(sec[:, i].mean()) for i, n in enumerate(names)},
        "wave_total_median": int(np.median(st[:, 5] - st[:, 0])),
        "kernel_us_events": kern_us}
+tot = st[:, 5] - st[:, 0]
+order = np.argsort(tot)
+slow, fast = order[-max(1, W // 10):], order[:max(1, W // 10)]
+out["slowest10pct_cycles_median"] = {n: int(np.median(sec[slow, i])) for i, n in enumerate(names)}
+out["fastest10pct_cycles_median"] = {n: int(np.median(sec[fast, i])) for i, n in enumerate(names)}
+out["slowest10pct_xcd_hist"] = np.bincount(((slow // 4) % 8), minlength=8).tolist()
+out["total_cycles_pctl"] = [int(np.percentile(tot, p)) for p in (0, 10, 50, 90, 100)]
 if kern == "k_episode_jl":   # the epilogue runs in wave 0 of each workgroup
     out["cycles_median_wave0"] = {n: int(np.median(sec[::4, i])) for i, n in enumerate(names)}
 # s_memtime counters are per XCD (workgroup b runs on XCD b % 8): start / end spread inside each
