@@ -25,20 +25,21 @@ int fgx_launch_episode_jl(const fgx::DevCfg& c, const fgx::DevState& s, int mp, 
 
 namespace fgx {
 
-// Episode kernels: k_episode (fgx_kernels.h, one env per lane, every case), k_episode_jp (fgx_jp.h,
-// one wave per joint) and k_episode_ws (fgx_ws.h, trajectory-producer / dynamics-consumer wave
-// pairs).  The last two serve SimpleReacher + PD over the shared basis tables with static
-// replanning schedules, max_episode_steps <= 200 and no per-step info, bit-identically to
-// k_episode (tests/test_gpu_jp.py, tests/test_gpu_ws.py).  Which one runs follows the measured
-// table profiles/r01_jp_vs_classic.jsonl + profiles/r01_ws_scan.jsonl (every kernel forced over
-// envs per GPU x MP kind x links on one MI355X):
-//  * k_episode holds one wave (64 envs) per SIMD, so it takes ceil(N / (64 x 4 x CUs)) rounds of a
-//    near-fixed ~75-93 us (5 links): a lone wave issues only every ~6-9 cycles.
-//  * k_episode_jp grows ~linearly with N (5 links: ~1.65 us per 1k envs): it wins for 5 links while
-//    k_episode's single round is at most 3/4 full or its last round at most half full, and for
-//    DMP at every size (up to 2.7x).  Short replanning segments pay its per-chunk exchange.
-//  * k_episode_ws wins for 2-link ProDMP up to one full round (~10%, also with replanning).
-// FGX_EPISODE_KERNEL=classic|jp|ws forces a kernel wherever it applies (A/B benchmarks, tests).
+// Episode kernels: k_episode (fgx_kernels.h, one env per lane, every case), k_episode_jl (fgx_jl.h,
+// one lane per env x joint), k_episode_jp (fgx_jp.h, one wave per joint) and k_episode_ws
+// (fgx_ws.h, trajectory-producer / dynamics-consumer wave pairs).  The last three serve
+// SimpleReacher + PD over the shared basis tables with static replanning schedules,
+// max_episode_steps <= 200 and no per-step info, bit-identically to k_episode (tests/test_gpu_jl.py,
+// test_gpu_jp.py, test_gpu_ws.py).  Which one runs follows the measured table
+// profiles/r02_kernel_scan_all.jsonl (every kernel forced over envs per GPU x MP kind x links on one
+// MI355X, tools/scan_all.sh):
+//  * k_episode holds one wave (64 envs) per SIMD: a near-fixed ~73-105 us (5 links) up to one full
+//    round of 65536 envs, where its 5 independent joint chains per lane keep the lone wave busy;
+//  * k_episode_jl puts 5x the lanes to work below that (8192 envs: 26 us vs 41 us k_episode_jp and
+//    61 us k_episode, ProMP 5 links) and wins at every size for 2 links (the 2-link k_episode is a
+//    short-chain lone wave too), replanning included;
+//  * k_episode_jp keeps the 5-link cases past one round whose last round is at most half full.
+// FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel wherever it applies (A/B benchmarks, tests).
 enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
@@ -64,14 +65,9 @@ inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env
     if (std::strcmp(v, "jl") == 0) return EK_JL;
   }
   const int64_t R = round_envs(), tail = c.N % R;
-  if (c.nl == 5) {
-    if (c.replan) return EK_CLASSIC;
-    if (mp == MP_DMP) return EK_JP;
-    const bool jp = 4 * c.N <= 3 * R || (c.N > R && tail != 0 && 2 * tail <= R);
-    return jp ? EK_JP : EK_CLASSIC;
-  }
-  if (mp == MP_PRODMP && c.N <= R) return EK_WS;
-  if (mp == MP_DMP && !c.replan && c.N <= R) return EK_JP;
+  if (c.nl == 2) return EK_JL;
+  if (4 * c.N <= 3 * R) return EK_JL;
+  if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return EK_JP;
   return EK_CLASSIC;
 }
 

@@ -24,11 +24,15 @@ pytestmark = pytest.mark.gpu
 REPLAN25 = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
 # (label, env id, override, envs per GPU, BB steps, expected kernel)
 CONFIGS = [
-    ("config2", "fancy_ProMP/SimpleReacher-v0", None, 4096, 2, "k_episode"),
+    ("config2", "fancy_ProMP/SimpleReacher-v0", None, 4096, 2, "k_episode_jl"),
     ("config3", "fancy_ProDMP/HoleReacher-v0", None, 65536, 2, "k_episode"),
-    ("config4_shard", "fancy_DMP/LongSimpleReacher-v0", None, 32768, 2, "k_episode_jp"),
-    ("config5_shard", "fancy_ProDMP/SimpleReacher-v0", REPLAN25, 8192, 4, "k_episode_ws"),
+    ("config4_shard", "fancy_DMP/LongSimpleReacher-v0", None, 32768, 2, "k_episode_jl"),
+    ("config5_shard", "fancy_ProDMP/SimpleReacher-v0", REPLAN25, 8192, 4, "k_episode_jl"),
     ("metric", "fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode"),
+    # the metric's strong-scaling shards (65536 / G envs per GPU on G = 2, 4, 8 GPUs)
+    ("metric_shard2", "fancy_ProMP/LongSimpleReacher-v0", None, 32768, 2, "k_episode_jl"),
+    ("metric_shard4", "fancy_ProMP/LongSimpleReacher-v0", None, 16384, 2, "k_episode_jl"),
+    ("metric_shard8", "fancy_ProMP/LongSimpleReacher-v0", None, 8192, 2, "k_episode_jl"),
 ]
 
 

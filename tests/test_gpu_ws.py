@@ -56,9 +56,12 @@ def test_episode_kernel_selection():
     rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
     cases = [("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 0, "k_episode"),      # the metric config
              ("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode"),      # per-step info arrays
-             ("fancy_ProMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jp"),
-             ("fancy_DMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jp"),     # config 4 shard
-             ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_ws"),         # config 5 shard
+             ("fancy_ProMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),   # metric shards
+             ("fancy_ProMP/LongSimpleReacher-v0", None, 8192, 0, "k_episode_jl"),
+             ("fancy_ProMP/LongSimpleReacher-v0", None, 98304, 0, "k_episode_jp"),   # half-full 2nd round
+             ("fancy_DMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),     # config 4 shard
+             ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_jl"),         # config 5 shard
+             ("fancy_ProMP/SimpleReacher-v0", None, 65536, 0, "k_episode_jl"),       # 2 links: every size
              ("fancy_ProDMP/HoleReacher-v0", None, 4096, 0, "k_episode")]
     for env_id, over, N, lvl, want in cases:
         env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
