@@ -21,6 +21,7 @@ import glob
 import json
 import os
 import re
+import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "fancy_ProMP/LongSimpleReacher-v0"
@@ -29,7 +30,7 @@ T = 200
 
 def kernel_family(name):
     """'fgx::k_episode_jp<1, 5, 5>(...)' -> 'k_episode_jp' (the name env.episode_kernel() reports)."""
-    m = re.search(r"(k_episode(?:_jp|_ws)?)\b", name)
+    m = re.search(r"(k_episode(?:_jp|_ws|_jl)?)\b", name)
     return m.group(1) if m else None
 
 
@@ -66,7 +67,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("--round", default="r02")
+    ap.add_argument("--build-id", default=None, help="build id of the profiled library (default: the "
+                    "hash of the sources in this tree)")
     a = ap.parse_args()
+    bid = a.build_id or build_id()
     entries = []
     for d in sorted(glob.glob(os.path.join(a.src, "n*"))):
         envs = int(os.path.basename(d)[1:])
@@ -79,7 +83,7 @@ def main():
         if fam is None:
             continue
         e = {"workload": WORKLOAD, "envs": envs, "kernel": fam, "kernel_name": full,
-             "build_id": build_id(), "kernel_ns_median_under_pmc": ns,
+             "build_id": bid, "kernel_ns_median_under_pmc": ns,
              "counters_per_dispatch": counters,
              "source": f"profiles/{a.round}_pmc/n{envs}"}
         if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
@@ -96,6 +100,13 @@ def main():
     out = {"method": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc_r02.sh); median over "
                      "dispatches of the per-dispatch sum over instances; traffic = (2*FETCH_SIZE + "
                      "WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count)", "entries": entries}
+    # the counter CSVs the entries come from travel with the summary
+    for d in sorted(glob.glob(os.path.join(a.src, "n*"))):
+        for path in glob.glob(os.path.join(d, "*", "**", "*_counter_collection.csv"), recursive=True):
+            part = os.path.relpath(path, d).split(os.sep)[0]
+            dd = os.path.join(ROOT, "profiles", f"{a.round}_pmc", os.path.basename(d), part)
+            os.makedirs(dd, exist_ok=True)
+            shutil.copy(path, os.path.join(dd, os.path.basename(path)))
     dst = os.path.join(ROOT, "profiles", "pmc_summary.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
