@@ -16,6 +16,7 @@
 #include "fgx_aux.h"
 #include "fgx_dispatch.h"
 #include "fgx_learned.h"
+#include "fgx_step.h"
 
 using namespace fgx;
 
@@ -135,8 +136,6 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     return fail(FGX_E_INVALID, "learn_sub_trajectories requires learn_tau");
   if ((c.learn_tau || c.learn_delay) && c.mp_kind == FGX_MP_NONE)
     return fail(FGX_E_INVALID, "learn_tau / learn_delay need a movement primitive");
-  if (c.learn_delay && c.mp_kind == FGX_MP_PRODMP)
-    return fail(FGX_E_UNSUPPORTED, "prodmp with a learned delay");
   if (c.learn_tau && !(c.tau_bound_lo > 0.0 && c.tau_bound_lo <= c.tau_bound_hi))
     return fail(FGX_E_INVALID, "tau_bound must satisfy 0 < lo <= hi");
   if (c.learn_delay && !(c.delay_bound_lo >= 0.0 && c.delay_bound_lo <= c.delay_bound_hi))
@@ -152,7 +151,6 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
       return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14
-    if (c.mp_kind == FGX_MP_PRODMP && c.delay != 0.0) return fail(FGX_E_UNSUPPORTED, "prodmp with delay");
     if (!(c.tau > 0.0) || !(c.dt > 0.0)) return fail(FGX_E_INVALID, "tau/dt must be positive");
   }
   if (c.time_aware && c.return_context) return fail(FGX_E_INVALID, "time_aware with context observation");
@@ -367,8 +365,8 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   } else if (d.mp == MP_PRODMP) {
     e = hipMalloc(&h->scratch, sizeof(double) * d.rows * 2 * d.nb + 64);
     if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_NOMEM, "hipMalloc scratch"); }
-    hipLaunchKernelGGL(k_tables_prodmp, dim3(1), dim3(256), 0, 0, d, cfg->tau, cfg->alpha_phase, cfg->bandwidth,
-                       h->scratch, h->tables);
+    hipLaunchKernelGGL(k_tables_prodmp, dim3(1), dim3(256), 0, 0, d, cfg->tau, cfg->delay, cfg->alpha_phase,
+                       cfg->bandwidth, h->scratch, h->tables);
   }
   if (d.mp != MP_NONE && d.rows > 0) {
     const int n = tables_t_rows(d.rows) * d.stride;
@@ -536,20 +534,24 @@ int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward,
   Handle* h = (Handle*)handle;
   if (!h) return fail(FGX_E_INVALID, "null handle");
   if (!actions || !obs || !reward || !terminated || !truncated) return fail(FGX_E_INVALID, "null argument");
-  const int threads = 256;
+  if (h->dc.time_aware) return fail(FGX_E_UNSUPPORTED, "step-based envs have no TimeAwareObservation");
+  const int threads = kStepRawBlock;
   const int blocks = (int)((h->dc.N + threads - 1) / threads);
   hipStream_t s = (hipStream_t)stream;
+  // LDS rows of the workgroup's action / observation slices (k_step_raw)
+  const int so = step_raw_stride(h->dc.obs_dim), sa = step_raw_stride(h->dc.nl);
+  const size_t lds = sizeof(float) * threads * ((so > sa ? so : sa) + (final_obs ? so : 0));
 #define X(NL)                                                                                                  \
   if (h->dc.nl == NL) {                                                                                        \
     if (h->dc.env == ENV_SIMPLE)                                                                               \
-      hipLaunchKernelGGL((k_step_raw<ENV_SIMPLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions, \
-                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+      hipLaunchKernelGGL((k_step_raw<ENV_SIMPLE, NL>), dim3(blocks), dim3(threads), lds, s, h->dc, h->st,        \
+                         actions, obs, reward, terminated, truncated, final_obs, autoreset);                   \
     else if (h->dc.env == ENV_HOLE)                                                                            \
-      hipLaunchKernelGGL((k_step_raw<ENV_HOLE, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions,   \
-                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+      hipLaunchKernelGGL((k_step_raw<ENV_HOLE, NL>), dim3(blocks), dim3(threads), lds, s, h->dc, h->st,          \
+                         actions, obs, reward, terminated, truncated, final_obs, autoreset);                   \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_step_raw<ENV_VIA, NL>), dim3(blocks), dim3(threads), 0, s, h->dc, h->st, actions,    \
-                         obs, reward, terminated, truncated, final_obs, autoreset);                            \
+      hipLaunchKernelGGL((k_step_raw<ENV_VIA, NL>), dim3(blocks), dim3(threads), lds, s, h->dc, h->st,           \
+                         actions, obs, reward, terminated, truncated, final_obs, autoreset);                   \
     HIP_TRY(hipGetLastError());                                                                                \
     return FGX_OK;                                                                                             \
   }

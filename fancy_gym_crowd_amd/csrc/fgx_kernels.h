@@ -8,7 +8,6 @@
 //                 clip, reacher dynamics, FK, collisions, reward, TimeLimit, replanning and the
 //                 numpy-pairwise return, with env state in registers for all T substeps, then
 //                 the VectorEnv auto-reset — one launch per BB step.
-//   k_step_raw    one step-based env.step for all envs (the per-substep kernel)
 //   k_traj_valu   desired trajectories [N, T, dof] (reference path for k_traj_mfma)
 //   k_traj_mfma   desired trajectories as an f32 MFMA GEMM (v_mfma_f32_32x32x2_f32)
 #pragma once
@@ -1059,38 +1058,6 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
   FGX_STAMP(o, e, 5);
   FGX_STAMP(o, e, 7);
-}
-
-// ============================================================================ step-based
-template <int ENV, int NL>
-__global__ __launch_bounds__(256) void k_step_raw(DevCfg c, DevState s, const float* __restrict__ act, float* obs,
-                                                  double* rew, uint8_t* term, uint8_t* trunc, float* final_obs,
-                                                  int autoreset) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= c.N) return;
-  const int64_t N = c.N;
-  Env<NL> v;
-  load_env(c, s, e, v);
-  float a32[NL];
-  double a[NL];
-#pragma unroll
-  for (int d = 0; d < NL; ++d) { a32[d] = act[e * NL + d]; a[d] = (double)a32[d]; }
-  const StepOut r = substep<ENV, true, NL>(c, v, a, a32, true);
-  const bool te = (ENV != ENV_SIMPLE) && r.coll, tr = v.steps >= c.max_steps;
-  rew[e] = r.reward;
-  term[e] = te;
-  trunc[e] = tr;
-  float* ob = obs + e * c.obs_dim;
-  float* fo = final_obs ? final_obs + e * c.obs_dim : nullptr;
-  if (autoreset && (te || tr)) {
-    if (fo) emit_obs(c, v, false, fo, nullptr);
-    autoreset_env(c, s, e, v);
-    v.flags = 0;
-    emit_obs(c, v, false, ob, nullptr);
-  } else {
-    emit_obs(c, v, false, ob, fo);
-  }
-  store_env(c, s, e, v);
 }
 
 // ============================================================================ trajectories

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void k_traj_env(DevCfg c, DevState s, const fl
   float* tab = env_tab + (size_t)e * c.rows * c.stride;
   const int R = s0 + Te + 2;
   if (MP == MP_PRODMP) {
-    prodmp_rows_seq(c, tau, c.alpha_phase, c.bandwidth, R, tab);
+    prodmp_rows_seq(c, tau, delay, c.alpha_phase, c.bandwidth, R, tab);
   } else {
     for (int i = s0; i < R; ++i) rbf_row(c, i, tau, delay, c.alpha_phase, c.bandwidth, tab + (size_t)i * c.stride);
   }

@@ -112,9 +112,21 @@ __device__ inline void prodmp_row(const DevCfg& c, double s, const double* p1, c
   row[2 * nb + 5] = (float)dy2;
 }
 
+// ProDMP with a delay: the basis is looked up on the left-bounded linear phase, fine-grid index
+// j(i) = rint(max((t_i - delay) / tau, 0) / (dt / tau)) for t_i = i dt (oracle/mp.py:
+// prodmp_delay_index): rows before the delay all equal the s = 0 row, so the plan holds its
+// initial position and velocity there (test_black_box.py:267-307).  j(i) <= i, non-decreasing.
+__device__ inline int prodmp_delay_index(const DevCfg& c, int i, double tau, double delay) {
+  double u = ((double)i * c.dt - delay) / tau;
+  u = u > 0.0 ? u : 0.0;
+  return (int)rint(u / (c.dt / tau));
+}
+
 // One env's ProDMP rows 0..R-1 for its own tau, sequentially in one thread (the cumulative
-// trapezoid in the same order as k_tables_prodmp / the oracle).
-__device__ inline void prodmp_rows_seq(const DevCfg& c, double tau, double alpha_x, double bw, int R, float* tab) {
+// trapezoid in the same order as k_tables_prodmp / the oracle), then the delay remap in place
+// (descending i: row j(i) <= i is still the fine-grid row when row i is written).
+__device__ inline void prodmp_rows_seq(const DevCfg& c, double tau, double delay, double alpha_x, double bw, int R,
+                                       float* tab) {
   const int nb = c.nb;
   const double h = c.dt / tau;
   double p1[kMaxBasis], p2[kMaxBasis], prev1[kMaxBasis], prev2[kMaxBasis], cur1[kMaxBasis], cur2[kMaxBasis];
@@ -132,10 +144,17 @@ __device__ inline void prodmp_rows_seq(const DevCfg& c, double tau, double alpha
     }
     prodmp_row(c, s, p1, p2, tab + (size_t)i * c.stride);
   }
+  if (delay != 0.0)
+    for (int i = R - 1; i > 0; --i) {
+      const int j = prodmp_delay_index(c, i, tau, delay);
+      if (j != i)
+        for (int k = 0; k < c.stride; ++k) tab[(size_t)i * c.stride + k] = tab[(size_t)j * c.stride + k];
+    }
 }
 
 // ProDMP precompute (oracle/mp.py:prodmp_fine64).  Single block; scratch: [rows][2*nb] f64.
-__global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw, double* dp, float* tab) {
+__global__ void k_tables_prodmp(DevCfg c, double tau, double delay, double alpha_x, double bw, double* dp,
+                                float* tab) {
   const int nb = c.nb, R = c.rows, W = 2 * nb;
   const double h = c.dt / tau;
   for (int i = threadIdx.x; i < R; i += blockDim.x)
@@ -154,8 +173,10 @@ __global__ void k_tables_prodmp(DevCfg c, double tau, double alpha_x, double bw,
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < R; i += blockDim.x)
-    prodmp_row(c, (double)i * h, dp + (size_t)i * W, dp + (size_t)i * W + nb, tab + (size_t)i * c.stride);
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {   // row i = fine-grid row j(i) (delay)
+    const int j = delay != 0.0 ? prodmp_delay_index(c, i, tau, delay) : i;
+    prodmp_row(c, (double)j * h, dp + (size_t)j * W, dp + (size_t)j * W + nb, tab + (size_t)i * c.stride);
+  }
 }
 
 // column-major copy of the shared table (DevState::tables_t)

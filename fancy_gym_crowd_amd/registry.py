@@ -474,8 +474,6 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     db = ph.get('delay_bound') or [0, duration - c.dt * 2]
     c.tau_bound_lo, c.tau_bound_hi = float(tb[0]), float(tb[1])
     c.delay_bound_lo, c.delay_bound_hi = float(db[0]), float(db[1])
-    if learn_delay and tg_type == 'prodmp':
-        raise NotImplementedError("ProDMP with learn_delay")
     # reward_aggregation (black_box_wrapper.py:252): np.sum / np.mean run in the episode kernel
     # (numpy's pairwise sum); any other callable is applied to each env's rewards[:t+1]
     agg = bb.get('reward_aggregation', np.sum)

@@ -163,8 +163,22 @@ def build_tables(spec, n_rows):
         return dict(psi=psi, sdt=(s32[1:] - s32[:-1]).astype(f32))
     if spec.kind == "prodmp":
         fine = prodmp_fine64(spec, n_rows)
+        if spec.delay:
+            j = prodmp_delay_index(spec, t[:n_rows])
+            fine = {k: v[j] for k, v in fine.items()}
         return {k: v.astype(f32) for k, v in fine.items()}
     raise ValueError(spec.kind)
+
+
+def prodmp_delay_index(spec, t):
+    """ProDMP with a delay: fine-grid index of time t on the left-bounded linear phase,
+    rint(max((t - delay) / tau, 0) / (dt / tau)) — mp_pytorch's ProDMP basis looks its
+    precomputed rows up at the rounded scaled-time index of the (delay-shifted, clamped at 0)
+    linear phase.  Parity unpinned like the rest of this module; what the reference's tests pin
+    for a ProDMP delay (constant position and velocity before the delay, moving after,
+    test_black_box.py:267-307) is re-checked in tests/test_mp_structure.py."""
+    u = np.maximum((np.asarray(t, np.float64) - spec.delay) / spec.tau, 0.0)
+    return np.rint(u / (spec.dt / spec.tau)).astype(np.int64)
 
 
 # ----------------------------------------------------------------------------- trajectories

@@ -495,6 +495,36 @@ def test_wall_collision_randomised_raw_steps(name, kw):
     assert n_coll > 100
 
 
+@pytest.mark.parametrize("name,N", [("SimpleReacher", 1000), ("LongSimpleReacher", 257), ("HoleReacher", 513)])
+def test_step_raw_ragged_vs_oracle(name, N):
+    """k_step_raw stages each workgroup's action / observation rows through LDS: env counts that
+    leave a partial last workgroup (1000 = 3·256 + 232, 257, 513), 205 steps so the TimeLimit
+    truncates and auto-resets every env once; final and reset observations, rewards, flags
+    and the whole f64 state vs the oracle."""
+    env = fgx.make(f"fancy/{name}-v0", num_envs=N, device=DEV)
+    o0, _ = env.reset(seed=5)
+    ob = batched.BatchedReacher(name, N)
+    close(np_(o0), ob.reset(list(range(N)), [5 + i for i in range(N)]))
+    rng = np.random.default_rng(8)
+    n = env.dof
+    for t in range(205):
+        a = rng.uniform(-20.0, 20.0, (N, n)).astype(np.float32)
+        obs, rew, te, tr, info = env.step(torch.from_numpy(a))
+        o_r, r_r, te_r, tr_r, _ = ob.step(a.astype(np.float64), np.ones(N, bool), True)
+        np.testing.assert_array_equal(np_(te).astype(bool), te_r)
+        np.testing.assert_array_equal(np_(tr).astype(bool), tr_r)
+        close(np_(rew), r_r)
+        close(np_(info["final_observation"]), o_r)
+        done = np.nonzero(te_r | tr_r)[0]
+        if len(done):
+            close(np_(obs)[done], ob.reset(list(done)))
+        if t % 50 == 0 or t == 204:
+            st = env.get_state()
+            np.testing.assert_array_equal(np_(st["q"]), ob.q)
+            np.testing.assert_array_equal(np_(st["qd"]), np.asarray(ob.qd, np.float64))
+            np.testing.assert_array_equal(np_(st["steps"]), ob.steps)
+
+
 def test_set_state_then_step_matches_oracle():
     """fgx_set_state (checkpoint restore): a BB step from an arbitrary restored state."""
     N = 192

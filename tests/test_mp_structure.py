@@ -115,26 +115,31 @@ def test_learn_tau_structure(kind, tau):
     assert np.all(pos[:k - 1] != pos[-1]) and np.all(vel[:k - 2] != vel[-1])
 
 
+@pytest.mark.parametrize("kind", ["promp", "prodmp"])
 @pytest.mark.parametrize("delay", [0, 0.25, 0.5, 0.75])
-def test_learn_delay_structure(delay):
-    """test_black_box.py:258-297 (ProMP): constant during the delay, moving after it."""
-    pos, vel, L = _learned("promp", "linear", [delay], dict(learn_delay=True))
+def test_learn_delay_structure(kind, delay):
+    """test_black_box.py:258-307 (ProMP, linear phase; ProDMP, exp phase): constant during the
+    delay, moving after it."""
+    pos, vel, L = _learned(kind, "linear" if kind == "promp" else "exp", [delay], dict(learn_delay=True))
     k = int(np.round(delay / 0.01))
     assert L == 200
     assert np.all(pos[:max(1, k - 1)] == pos[0]) and np.all(vel[:max(1, k - 2)] == vel[0])
     assert np.all(pos[max(1, k):] != pos[0]) and np.all(vel[max(1, k)] != vel[0])
 
 
+@pytest.mark.parametrize("kind", ["promp", "prodmp"])
 @pytest.mark.parametrize("tau", [0.25, 0.5, 0.75, 1.0])
 @pytest.mark.parametrize("delay", [0.25, 0.5, 0.75, 1.0])
-def test_learn_tau_and_delay_structure(tau, delay):
-    """test_black_box.py:300-368 (ProMP)."""
+def test_learn_tau_and_delay_structure(kind, tau, delay):
+    """test_black_box.py:310-368 (ProMP linear / ProDMP exp phase)."""
     if 2.0 < delay + tau:
         return
-    pos, vel, L = _learned("promp", "linear", [tau, delay], dict(learn_tau=True, learn_delay=True))
+    pos, vel, L = _learned(kind, "linear" if kind == "promp" else "exp", [tau, delay],
+                           dict(learn_tau=True, learn_delay=True))
     kt, kd = int(np.round(tau / 0.01)), int(np.round(delay / 0.01))
     kj = kt + kd
-    assert np.all(pos[kj:] == pos[-1]) and np.all(vel[kj:] == vel[-1])
+    if kind == "promp":   # flat end only for the linear phase
+        assert np.all(pos[kj:] == pos[-1]) and np.all(vel[kj:] == vel[-1])
     assert np.all(pos[:kd - 1] == pos[0]) and np.all(vel[:kd - 2] == vel[0])
     ap, av = pos[kd:kj - 1], vel[kd:kj - 2]
     assert np.all(ap != pos[-1]) and np.all(ap != pos[0])

@@ -83,24 +83,31 @@ def trajectory(env_id, N, force_valu=False):
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
 
-def step_raw(env_id, N):
+def step_raw(env_id, N, final_obs=True):
+    """k_step_raw through fgx_step_raw as StepVectorEnv.step calls it (with final_obs)."""
     env = fgx.make(env_id, num_envs=N, device=dev, info_level=0)
     env.reset(seed=0)
-    n = env.dof
+    n, od = env.dof, env.obs_dim
     a = (torch.rand((N, n), device=dev) * 2 - 1) * 10
-    obs = torch.empty((N, env.obs_dim), device=dev)
+    obs = torch.empty((N, od), device=dev)
+    fobs = torch.empty((N, od), device=dev)
     rew = torch.empty(N, dtype=torch.float64, device=dev)
     te = torch.empty(N, dtype=torch.uint8, device=dev)
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     import ctypes
     lib, h = env._eng.lib, env._eng.h
     args = [ctypes.c_void_p(x.data_ptr()) for x in (a, obs, rew, te, tr)]
-    t = timed(lambda: lib.fgx_step_raw(h, *args, None, 1, env._eng.stream()), reps=50)
-    # algorithmic bytes per env-step: action in, state r/w, obs out, reward, flags
-    state = 2 * n * 8 * 2 + 16 + 24 + 12 * 2
-    b = N * (n * 4 + state + env.obs_dim * 4 + 8 + 2)
-    print(json.dumps(dict(kernel="k_step_raw", config=env_id, envs=N, kernel_us=t * 1e6, steps_per_s=N / t,
-                          GBps=b / t / 1e9, hbm_frac=b / t / 8e12)), flush=True)
+    fo = ctypes.c_void_p(fobs.data_ptr()) if final_obs else None
+    t = timed(lambda: lib.fgx_step_raw(h, *args, fo, 1, env._eng.stream()), reps=50)
+    # algorithmic bytes per env-step: action in; q, qd, goal, steps, flags (+ hole x / width /
+    # depth for Hole / ViaPoint) read and written; obs (+ final obs), reward, two flags out
+    # (the PCG64 state moves only on the 1-in-200 auto-reset)
+    hole = 0 if env_id.startswith("fancy/Simple") or env_id.startswith("fancy/LongSimple") else 24
+    state = 2 * n * 8 + 16 + 8 + hole
+    b = N * (n * 4 + 2 * state + od * 4 * (2 if final_obs else 1) + 8 + 2)
+    print(json.dumps(dict(kernel="k_step_raw", config=env_id, envs=N, final_obs=final_obs, kernel_us=t * 1e6,
+                          steps_per_s=N / t, bytes_per_env_step=b // N, GBps=b / t / 1e9, hbm_frac=b / t / 8e12,
+                          build=fgx._lib.load().fgx_build_id().decode())), flush=True)
 
 
 if __name__ == "__main__":
@@ -169,7 +176,10 @@ if __name__ == "__main__":
         for force in (False, True):
             trajectory("fancy_ProMP/LongSimpleReacher-v0", 65536, force)
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
-    if "raw" in which:
+    if "raw" in which:   # config 1 (step-based SimpleReacher) and the other step ids at 1M envs
+        for env_id in ("fancy/SimpleReacher-v0", "fancy/LongSimpleReacher-v0", "fancy/HoleReacher-v0",
+                       "fancy/ViaPointReacher-v0"):
+            step_raw(env_id, 1 << 20)
+        step_raw("fancy/SimpleReacher-v0", 1 << 20, final_obs=False)
+    if "raw1" in which:   # config 1 alone (PMC passes)
         step_raw("fancy/SimpleReacher-v0", 1 << 20)
-        step_raw("fancy/LongSimpleReacher-v0", 1 << 20)
-        step_raw("fancy/HoleReacher-v0", 1 << 20)
