@@ -38,8 +38,11 @@ namespace fgx {
 //  * k_episode_jl puts 5x the lanes to work below that (8192 envs: 26 us vs 41 us k_episode_jp and
 //    61 us k_episode, ProMP 5 links) and wins at every size for 2 links (the 2-link k_episode is a
 //    short-chain lone wave too), replanning included;
-//  * k_episode_jp keeps the 5-link cases past one round whose last round is at most half full.
-// FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel wherever it applies (A/B benchmarks, tests).
+//  * past one round whose last round is at most half full (5 links), k_episode_jl again (98304 envs:
+//    112 us vs 127 us k_episode, profiles/r02_jl_scan.jsonl; it took k_episode_jp's place there once
+//    its exchange rows stopped conflicting on LDS banks).
+// k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
+// wherever it applies (A/B benchmarks, tests).
 enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
@@ -67,7 +70,7 @@ inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env
   const int64_t R = round_envs(), tail = c.N % R;
   if (c.nl == 2) return EK_JL;
   if (4 * c.N <= 3 * R) return EK_JL;
-  if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return EK_JP;
+  if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return EK_JL;
   return EK_CLASSIC;
 }
 

@@ -52,8 +52,17 @@ struct JlShape {
   // gathered f64 per env: A, B, tail (8 each), cfk, q, qd, then cos / sin of the cumulative angles
   // (FK) and of every q (observation)
   static constexpr int GF = 25 + 6 * NL;
+  // row stride (doubles) of the a^2 exchange rows.  The owner lane of slot j reads a^2 of joint dd
+  // of env g at row j, column g NL + dd; with 64-double rows every row starts on the same bank, so
+  // the NL lanes of one env (rows d, d + NL, ...) hit one bank pair: 5-way conflicts for 5 links
+  // (PMC SQ_LDS_BANK_CONFLICT = 63% of SQ_LDS_IDX_ACTIVE at 65536 envs,
+  // profiles/r02_stall_probe.json).  An odd stride spreads the rows over the banks (modelled
+  // ds_read_b64 group cycles per chunk, tools/lds_bank_model.py): 5 links use 60 columns, stride 61
+  // (90 -> 40, the LDS footprint shrinks; the 4 idle lanes do not write), 2 links stride 65
+  // (32 -> 16, conflict-free; the gather area is larger anyway).  Writes stay conflict-free.
+  static constexpr int XS = (G * NL < 64) ? G * NL + 1 : 65;
   static constexpr size_t lds_bytes() {
-    const size_t ex = (size_t)WAVES * 16 * 64 * sizeof(double);
+    const size_t ex = (size_t)WAVES * 16 * XS * sizeof(double);
     const size_t ga = (size_t)GF * EPB * sizeof(double);
     return ex > ga ? ex : ga;
   }
@@ -78,7 +87,8 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   extern __shared__ double lds_jl[];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  double* ex = lds_jl + w * (16 * 64);  // this wave's two chunk buffers: a^2 of sample j at [j * 64 + lane]
+  constexpr int XS = S::XS;
+  double* ex = lds_jl + w * (16 * XS);  // this wave's two chunk buffers: a^2 of sample j at [j * XS + lane]
   const int g = lane / NL, d = lane - g * NL;
   const int64_t N = c.N;
   const int slot = w * G + g;           // LDS slot of this lane's env
@@ -171,21 +181,23 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   for (int sl = 0; sl < SPW; ++sl) { A[sl] = -0.0; B[sl] = -0.0; Tl[sl] = 0.0; }   // -0.0 + r == r
   const int gr = g < G ? g : G - 1;   // idle lanes read (and discard) the last env's rows
   auto write_sq = [&](int ch, const double* sq) __attribute__((always_inline)) {
-    double* b = ex + (ch & 1) * 512;
+    double* b = ex + (ch & 1) * (8 * XS);
+    if (G * NL == 64 || lane < G * NL) {   // (rows hold G NL columns: idle lanes must not write)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) b[j * 64 + lane] = sq[j];
+      for (int j = 0; j < 8; ++j) b[j * XS + lane] = sq[j];
+    }
   };
   // sum_d a_d^2 in joint order, the reward 0 - ctrl (rdist = 0 below env step 199) and numpy's
   // pairwise slots, branch-free (selects); chunk ch < 0 changes nothing
   auto reduce = [&](int ch) __attribute__((always_inline)) {
-    const double* b = ex + (ch & 1) * 512;
+    const double* b = ex + (ch & 1) * (8 * XS);
 #pragma unroll
     for (int sl = 0; sl < SPW; ++sl) {
       const int j = d + NL * sl;
       const bool ok = j < 8 && ch >= 0;
       const int jj = j < 8 ? j : 0;
       const int k = ch * 8 + jj;
-      const double* row = b + jj * 64 + gr * NL;
+      const double* row = b + jj * XS + gr * NL;
       double ctrl = row[0];
 #pragma unroll
       for (int dd = 1; dd < NL; ++dd) ctrl = fadd(ctrl, row[dd]);
@@ -301,12 +313,12 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     }
   };
   auto reduce_load = [&](int ch, double (*rv)[NL]) __attribute__((always_inline)) {
-    const double* b = ex + (ch & 1) * 512;
+    const double* b = ex + (ch & 1) * (8 * XS);
 #pragma unroll
     for (int sl = 0; sl < SPW; ++sl) {
       const int j = d + NL * sl;
       const int jj = j < 8 ? j : 0;   // (lanes without this slot accumulate a discarded sum)
-      const double* row = b + jj * 64 + gr * NL;
+      const double* row = b + jj * XS + gr * NL;
 #pragma unroll
       for (int dd = 0; dd < NL; ++dd) rv[sl][dd] = row[dd];
     }

@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 JL_CASES = CASES + [
     ("fancy_ProMP/LongSimpleReacher-v0", None, 61, 2),       # one partial workgroup, idle lanes
     ("fancy_ProMP/LongSimpleReacher-v0", None, 8193, 2),     # the 8-GPU shard size + 1
+    ("fancy_ProMP/LongSimpleReacher-v0", None, 98304, 2),    # dispatched past one round (half-full tail)
     ("fancy_ProMP/SimpleReacher-v0", None, 4097, 2),
     ("fancy_DMP/LongSimpleReacher-v0", {"basis_generator_kwargs": {"num_basis": 3}}, 97, 2),
     ("fancy_ProDMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}}, 150, 6),

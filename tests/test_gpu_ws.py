@@ -58,7 +58,7 @@ def test_episode_kernel_selection():
              ("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode"),      # per-step info arrays
              ("fancy_ProMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),   # metric shards
              ("fancy_ProMP/LongSimpleReacher-v0", None, 8192, 0, "k_episode_jl"),
-             ("fancy_ProMP/LongSimpleReacher-v0", None, 98304, 0, "k_episode_jp"),   # half-full 2nd round
+             ("fancy_ProMP/LongSimpleReacher-v0", None, 98304, 0, "k_episode_jl"),   # half-full 2nd round
              ("fancy_DMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),     # config 4 shard
              ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_jl"),         # config 5 shard
              ("fancy_ProMP/SimpleReacher-v0", None, 65536, 0, "k_episode_jl"),       # 2 links: every size

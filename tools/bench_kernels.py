@@ -163,6 +163,9 @@ if __name__ == "__main__":
             episode("fancy_ProMP/LongSimpleReacher-v0", n, label="scan: ProMP LongSimpleReacher", reps=10)
     if "metric" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
+    if "probe" in which:   # metric env at one full k_episode round and at the 2-GPU shard (PMC probes)
+        episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="probe 65536", reps=10)
+        episode("fancy_ProMP/LongSimpleReacher-v0", 32768, label="probe 32768", reps=10)
     if "episode" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
         episode("fancy_ProMP/LongSimpleReacher-v0", 262144, label="ProMP LongSimpleReacher x4 envs")
