@@ -163,6 +163,14 @@ if __name__ == "__main__":
             episode("fancy_ProMP/LongSimpleReacher-v0", n, label="scan: ProMP LongSimpleReacher", reps=10)
     if "metric" in which:
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="metric: ProMP LongSimpleReacher")
+    if "shards" in which:   # the metric's strong-scaling shards (1/2/4/8 GPUs) and configs 2 / 4 / 5
+        for n in (65536, 32768, 16384, 8192):
+            episode("fancy_ProMP/LongSimpleReacher-v0", n, label=f"shard {n}: ProMP LongSimpleReacher")
+        episode("fancy_ProMP/SimpleReacher-v0", 4096, label="config2: ProMP SimpleReacher")
+        episode("fancy_DMP/LongSimpleReacher-v0", 32768, label="config4: DMP LongSimpleReacher (1/8 shard)")
+        episode("fancy_ProDMP/SimpleReacher-v0", 8192,
+                over={"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}},
+                label="config5: ProDMP SimpleReacher replan 25 (1/8 shard)")
     if "probe" in which:   # metric env at one full k_episode round and at the 2-GPU shard (PMC probes)
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="probe 65536", reps=10)
         episode("fancy_ProMP/LongSimpleReacher-v0", 32768, label="probe 32768", reps=10)
