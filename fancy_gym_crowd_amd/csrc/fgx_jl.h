@@ -489,7 +489,14 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   }
   __syncthreads();
 
-  // ---- one thread per env: return and epilogue
+  // ---- one thread per env: return and epilogue (threads t < EPB).  The VectorEnv auto-reset of a
+  // truncated env depends only on its RNG stream and start angle, not on the episode, so when the
+  // workgroup has a second group of EPB threads (R0 = EPB rounded up to whole waves) those threads
+  // reset the envs in parallel (the PCG64 draws, the goal's rejection loops, FK of the fresh arm
+  // and its observation: most of the epilogue's instructions), while the first group forms the
+  // returns and final observations.  The second group starts after a barrier that follows the
+  // first group's reads of the same env state (JpSeg, load_env), so its reset stores cannot overtake
+  // them; before it, it only decides which of its envs truncate.
   const int t = threadIdx.x;
   const int tw = t / G, tg_ = t - tw * G;   // slot t = tw * G + tg_
   const int64_t et = (int64_t)blockIdx.x * (S::WAVES * gw) + tw * gw + tg_;
@@ -503,15 +510,42 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (lane == 0 && sum != 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
   }
   FGX_STAMP(o, wst, 4);
+  constexpr int R0 = (EPB + 63) / 64 * 64;
+  constexpr bool SPLIT = R0 + EPB <= 64 * S::WAVES;
+  const bool split = SPLIT && o.autoreset;
+  Env<NL> vr;
+  bool rs_do = false;
+  int64_t er = 0;
+  if (split) {
+    const int t1 = t - R0, tw1 = t1 / G, tg1 = t1 - tw1 * G;
+    er = (int64_t)blockIdx.x * (S::WAVES * gw) + tw1 * gw + tg1;
+    if (t1 >= 0 && t1 < EPB && tg1 < gw && er < N) {
+      JpSeg sr;
+      sr.init(c, s, er, true);
+      rs_do = sr.steps + sr.L >= c.max_steps;   // the segment ends in truncation (SimpleReacher never terminates)
+    }
+  }
+  JpSeg st;
+  Env<NL> v;
+  if (tv) {
+    st.init(c, s, et, true);
+    load_env(c, s, et, v, false);   // SimpleReacher: no hole / reward state
+  }
+  if (split) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state reads above have landed
+    __syncthreads();
+    if (rs_do) {   // concurrent with the first group's returns and final observations
+      autoreset_env(c, s, er, vr);
+      emit_obs(c, vr, c.return_context, o.obs + er * c.out_dim, nullptr, true);
+      store_env(c, s, er, vr, false);
+      s.plans[er] = 0;
+    }
+  }
   if (!tv) {
     FGX_STAMP(o, wst, 5);
     FGX_STAMP(o, wst, 7);
     return;
   }
-  JpSeg st;
-  st.init(c, s, et, true);
-  Env<NL> v;
-  load_env(c, s, et, v, false);   // SimpleReacher: no hole / reward state
 #pragma unroll
   for (int k = 0; k < NL; ++k) { v.q[k] = ga[(25 + k) * EPB + t]; v.qd[k] = ga[(25 + NL + k) * EPB + t]; }
   v.steps = st.steps + st.L;
@@ -542,7 +576,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (j < ntail) res = res + ((fk_last && j == ntail - 1) ? r_fk : ga[(3 * j + 2) * EPB + t]);
   if (L > 128) res = PairwiseSum::comb(sa) + res;
   const bool trunc = v.steps >= c.max_steps;
-  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_);
+  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_, split);
   FGX_STAMP(o, wst, 5);
   FGX_STAMP(o, wst, 7);
 }

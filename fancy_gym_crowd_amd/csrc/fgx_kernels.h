@@ -603,12 +603,13 @@ __device__ inline bool state_replan(const DevCfg& c, const Env<NL>& v) {
 
 // BB-step outputs, VectorEnv auto-reset and state write-back of one env (black_box_wrapper.py:
 // 241-253; gymnasium SyncVectorEnv autoreset), shared by k_episode and k_episode_jp.  v holds
-// the env after its last sample with FK refreshed.
+// the env after its last sample with FK refreshed.  reset_elsewhere (k_episode_jl): an ending env
+// only gets its outputs and final observation here; another wave runs its reset.
 template <int NL>
 __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState& s, const Outputs& o, int64_t e,
                                                  Env<NL>& v, int plans, int L, double ret, bool term, bool trunc,
                                                  bool count = true, const double* gcs = nullptr,
-                                                 const double* gsn = nullptr) {
+                                                 const double* gsn = nullptr, bool reset_elsewhere = false) {
   const int64_t N = c.N;
   o.ret[e] = ret;
   o.term[e] = term;
@@ -628,6 +629,7 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
   if (o.autoreset && (term || trunc)) {
     if (fo) emit_obs(c, v, c.return_context, fo, nullptr, false, true, gcs, gsn);
+    if (reset_elsewhere) return;   // another thread resets the env and writes its state / obs row
     autoreset_env(c, s, e, v);
     plans = 0;
     v.flags = 0;

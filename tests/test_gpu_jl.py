@@ -125,3 +125,28 @@ def test_jl_inner_steps_counter():
             os.environ.pop("FGX_EPISODE_KERNEL", None)
         else:
             os.environ["FGX_EPISODE_KERNEL"] = old
+
+
+@pytest.mark.parametrize("N", [1000, 8192])
+def test_jl_equals_classic_split_autoreset(N, monkeypatch):
+    """The auto-reset of truncated envs runs on a second thread group of each jl workgroup, beside the
+    returns / final observations of the first (fgx_jl.h epilogue): random_start False (the start
+    angle is restored, base_reacher.py:77-93) with envs at every env step, so only some envs of a
+    workgroup truncate; jl and k_episode agree bit for bit, state included."""
+    env_id = "fancy_ProMP/LongSimpleReacher-v0"
+    rng = np.random.default_rng(91)
+    params = [rng.standard_normal((N, 25), dtype=np.float32) for _ in range(3)]
+    outs = []
+    for kern in ("jl", "classic"):
+        monkeypatch.setenv("FGX_EPISODE_KERNEL", kern)
+        env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, random_start=False)
+        out = [np_(env.reset(seed=17)[0])]
+        env.set_state(steps=(np.arange(N) % 200).astype(np.int32))
+        for p in params:
+            obs, ret, te, tr, info = env.step(torch.from_numpy(p).to(DEV))
+            out += [np_(obs), np_(ret), np_(te), np_(tr), np_(info["trajectory_length"]),
+                    np_(info["final_observation"])]
+            out += list(_state(env).values())
+        assert env.episode_kernel() == ("k_episode_jl" if kern == "jl" else "k_episode")
+        outs.append(out)
+    _same(outs[0], outs[1])
