@@ -587,3 +587,20 @@ def test_step_before_reset_raises():
     raw = fgx.make("fancy/SimpleReacher-v0", num_envs=8, device=DEV)
     with pytest.raises(fgx.ResetNeeded):
         raw.step(torch.zeros((8, 2)))
+
+
+@pytest.mark.parametrize("env_id,N", [("fancy_ProMP/LongSimpleReacher-v0", 4099), ("fancy_ProDMP/HoleReacher-v0", 4099),
+                                      ("fancy_ProMP/SimpleReacher-v0", 1000), ("fancy_ProDMP/SimpleReacher-v0", 65536)])
+def test_trajectory_mfma_equals_valu(env_id, N):
+    """k_traj_mfma (one contiguous [envs, T, dof] output region per wave, MFMA columns = (env, joint)
+    pairs) against k_traj_valu on the same plans (a replanning schedule that never fires before T
+    routes get_trajectory to the VALU kernel): bit for bit, partial last wave included."""
+    outs = []
+    for over in (None, {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}):
+        env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+        params = torch.from_numpy(np.random.default_rng(5).standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)
+        env.reset(seed=3)
+        outs.append([np_(x) for x in env.trajectory(params)])
+    for a, b in zip(outs[0], outs[1]):
+        assert a.shape == b.shape
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
