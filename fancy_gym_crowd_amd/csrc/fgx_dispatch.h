@@ -43,7 +43,7 @@ namespace fgx {
 //    its exchange rows stopped conflicting on LDS banks).
 // k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
 // wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3 };
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -56,13 +56,25 @@ inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave
   return r;
 }
 
+// k_episode or k_episode_w2: 5-link SimpleReacher without per-step info past one k_episode round
+// (two resident waves per SIMD, profiles/r02_w2_ab.jsonl); FGX_EPISODE_KERNEL=classic keeps k_episode
+inline bool w2_applies(const DevCfg& c, bool log) { return c.env == ENV_SIMPLE && c.nl == 5 && !log; }
+inline int classic_choice(const DevCfg& c, bool log) {
+  if (!w2_applies(c, log)) return EK_CLASSIC;
+  if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
+    if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
+    if (std::strcmp(v, "w2") == 0) return EK_CLASSIC_W2;
+  }
+  return c.N > round_envs() ? EK_CLASSIC_W2 : EK_CLASSIC;
+}
+
 inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env_plans) {
   const bool eligible = c.env == ENV_SIMPLE && mp != MP_GIVEN && mp != MP_NONE && c.ctrl == CTRL_PD && !log &&
                         !c.sched_state && c.T <= 256 && c.max_steps <= 200 && !per_env_plans && !c.learn_tau &&
                         !c.learn_delay && (c.nl == 2 || c.nl == 5);
-  if (!eligible) return EK_CLASSIC;
+  if (!eligible) return classic_choice(c, log);
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
-    if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
+    if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "w2") == 0) return classic_choice(c, log);
     if (std::strcmp(v, "jp") == 0) return EK_JP;
     if (std::strcmp(v, "ws") == 0) return EK_WS;
     if (std::strcmp(v, "jl") == 0) return EK_JL;
@@ -71,7 +83,7 @@ inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env
   if (c.nl == 2) return EK_JL;
   if (4 * c.N <= 3 * R) return EK_JL;
   if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return EK_JL;
-  return EK_CLASSIC;
+  return classic_choice(c, log);
 }
 
 template <int MP, int NL, int NB>
@@ -136,6 +148,16 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
+  }
+  if constexpr (ENV == ENV_SIMPLE && NL == 5) {
+    if (classic_choice(c, log) == EK_CLASSIC_W2 &&
+        (MP == MP_GIVEN || CTRL != CTRL_PD || episode_kernel_choice(c, MP, log, s.plan_len != nullptr) == EK_CLASSIC_W2)) {
+      hipLaunchKernelGGL((k_episode_w2<ENV, MP, CTRL, NL, NB, false>), dim3(blocks), dim3(threads), lds, stream, c,
+                         s, params, dpos, dvel, o);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) { err = std::string("k_episode_w2 launch: ") + hipGetErrorString(e); return -2; }
+      return 0;
+    }
   }
   if (log)
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), lds, stream, c, s,

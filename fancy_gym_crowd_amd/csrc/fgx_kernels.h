@@ -642,10 +642,12 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
 }
 
 // ============================================================================ the BB step
+// The body of k_episode (below) and k_episode_w2 (the same code compiled for two resident waves
+// per SIMD).
 template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
-__global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const float* __restrict__ params,
-                                                 const float* __restrict__ dpos, const float* __restrict__ dvel,
-                                                 Outputs o) {
+__device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s, const float* __restrict__ params,
+                                             const float* __restrict__ dpos, const float* __restrict__ dvel,
+                                             const Outputs& o) {
   extern __shared__ float lds_tab[];
   if (MP != MP_GIVEN) {
     const int n = c.rows * c.stride;
@@ -1060,6 +1062,25 @@ __global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const flo
   episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
   FGX_STAMP(o, e, 5);
   FGX_STAMP(o, e, 7);
+}
+
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
+__global__ __launch_bounds__(256) void k_episode(DevCfg c, DevState s, const float* __restrict__ params,
+                                                 const float* __restrict__ dpos, const float* __restrict__ dvel,
+                                                 Outputs o) {
+  episode_body<ENV, MP, CTRL, NL, NB, LOG>(c, s, params, dpos, dvel, o);
+}
+
+// k_episode capped at 256 registers (two resident waves per SIMD; the 5-link SimpleReacher body
+// spills ~30 registers outside its sample loop, the loop itself is unchanged).  Past one round of
+// 64-lane waves per SIMD (N > 65536 on 256 CUs) the second wave shares the SIMD's issue slots
+// instead of waiting for the next round: ProMP 5 links 131072 envs 139 -> 126 us, 262144 262 ->
+// 224 us; within one round the uncapped kernel is faster (76.0 vs 80.4 us at 65536).
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_episode_w2(
+    DevCfg c, DevState s, const float* __restrict__ params, const float* __restrict__ dpos,
+    const float* __restrict__ dvel, Outputs o) {
+  episode_body<ENV, MP, CTRL, NL, NB, LOG>(c, s, params, dpos, dvel, o);
 }
 
 // ============================================================================ trajectories

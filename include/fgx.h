@@ -224,7 +224,8 @@ int fgx_get_tables(void* handle, float* out, void* stream);
 
 /* The kernel fgx_step launches for this handle with the given info level (>= 2: per-step info
  * arrays): 0 = k_episode (one env per lane), 1 = k_episode_jp (one wave per joint),
- * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs); negative on error.
+ * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs), 3 = k_episode_jl (one lane
+ * per env x joint), 4 = k_episode_w2 (k_episode for two resident waves per SIMD); negative on error.
  * All three give bit-identical results; the choice follows measured speed (fgx_dispatch.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 

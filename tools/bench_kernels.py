@@ -171,6 +171,12 @@ if __name__ == "__main__":
         episode("fancy_ProDMP/SimpleReacher-v0", 8192,
                 over={"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}},
                 label="config5: ProDMP SimpleReacher replan 25 (1/8 shard)")
+    if "big" in which:   # k_episode past one round (two resident waves per SIMD or not)
+        for n in (65536, 131072, 262144):
+            episode("fancy_ProMP/LongSimpleReacher-v0", n, label=f"big {n}: ProMP LongSimpleReacher", reps=10)
+        for env_id in ("fancy_DMP/LongSimpleReacher-v0", "fancy_ProDMP/LongSimpleReacher-v0"):
+            for n in (65536, 131072):
+                episode(env_id, n, label=f"big {n}: {env_id}", reps=10)
     if "probe" in which:   # metric env at one full k_episode round and at the 2-GPU shard (PMC probes)
         episode("fancy_ProMP/LongSimpleReacher-v0", 65536, label="probe 65536", reps=10)
         episode("fancy_ProMP/LongSimpleReacher-v0", 32768, label="probe 32768", reps=10)
