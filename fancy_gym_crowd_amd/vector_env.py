@@ -369,8 +369,8 @@ class BlackBoxVectorEnv:
                                                self._eng.stream()))
 
     def episode_kernel(self, info_level=None):
-        """Name of the HIP kernel step() launches (fgx_episode_kernel): k_episode, k_episode_jp or
-        k_episode_ws; all three produce bit-identical results."""
+        """Name of the HIP kernel step() launches (fgx_episode_kernel): k_episode, k_episode_jp,
+        k_episode_ws, k_episode_jl or k_episode_w2; all five produce bit-identical results."""
         lvl = self.info_level if info_level is None else int(info_level)
         k = self._eng.lib.fgx_episode_kernel(self._eng.h, lvl)
         if k < 0:
