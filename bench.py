@@ -6,7 +6,9 @@ BASELINE.json's metric is quoted at N = 65536 envs in total over 1/2/4/8 GPUs: t
 STRONG scaling (--global-envs 65536, each of the N ranks owns 65536/N envs).  --envs gives every
 rank a fixed number of envs instead (weak scaling).  With N > 1 the strong-scaling line also
 carries a weak-scaling measurement (65536 envs per GPU) as a secondary field.
-For N > 1 launch with torch.distributed.run (one process per GPU); env shards are independent
+For N > 1, `bench.py --gpus N` starts the N ranks itself (torch.distributed.run as a child process,
+one process per GPU) unless a launcher already did (WORLD_SIZE set; it must equal --gpus); with
+fewer visible GPUs than ranks they share cuda:0 over gloo (rehearsal).  Env shards are independent
 (seeds = global env index, the rank's rows of the global parameter matrix), RCCL only gathers the
 final episode returns.  Prints ONE JSON line on rank 0.
 
@@ -31,27 +33,58 @@ GLOBAL_ENVS = 65536
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_VEC_PEAK_TF = 157.3   # MI355X_MICROARCH.md: Peak FP32 (vector / matrix f32)
 CLOCK_GHZ = 2.4            # MI355X peak engine clock (GRBM_GUI_ACTIVE / kernel time agrees, profiles/)
-# VALU issue: a SIMD issues one wave64 f64 VALU instruction per 4 clocks at best (16 lanes x 4
-# passes); tools/valu_rates.hip measures 4.68 cycles with >= 4 independent waves per SIMD and
-# 6.12 for a lone wave (profiles/r01_valu_rates.jsonl, v_fma_f64 chains)
-ISSUE_ARCH_CYCLES = 4.0
+# VALU issue, architectural (MI355X_MICROARCH.md, Execution model + per-instruction constants): a
+# wave64 VALU instruction occupies its SIMD-32 for 2 cycles (f32 / int / packed f32); an f64 op or a
+# conversion runs at the 78.6 TF f64 vector rate, 4 cycles.  The peak of a kernel is 1 / (its
+# PMC-weighted mean of these costs).  tools/valu_rates.hip measures what the hardware sustains
+# beside it: 4.68 cycles per f64 instruction with >= 4 independent waves per SIMD, 6.12 for a lone
+# wave (profiles/r01_valu_rates.jsonl) -- reported as secondary fields, never as the peak.
+ISSUE_F64_CYCLES = 4.0
+ISSUE_F32_CYCLES = 2.0
 ISSUE_SIMD_CYCLES = 4.68
 ISSUE_SINGLE_WAVE_CYCLES = 6.12
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
-def pmc_entry(env_id, n_envs, kernel):
-    """Committed rocprofv3 PMC summary of the kernel this run launches (tools/pmc_summary.py):
-    total VALU instructions and HBM bytes per launch; None if that kernel / size was not profiled."""
+def lib_build_id():
+    from fancy_gym_crowd_amd import _lib
+    return _lib.load().fgx_build_id().decode()
+
+
+def pmc_entry(env_id, n_envs, kernel, build_id):
+    """Committed rocprofv3 PMC summary (tools/pmc_summary.py) of the kernel this run launches, for
+    the library build that runs: VALU instructions (and their f64 / conversion mix) and HBM bytes
+    per launch.  Returns (entry or None, note)."""
     try:
         with open(PMC_SUMMARY) as f:
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
-        return None
+        return None, "no profiles/pmc_summary.json"
+    stale = None
     for e in entries:
         if e.get("workload") == env_id and int(e.get("envs", -1)) == n_envs and e.get("kernel") == kernel:
-            return e
-    return None
+            if e.get("build_id") == build_id:
+                return e, "pmc of this build"
+            stale = e.get("build_id")
+    if stale is not None:
+        return None, f"pmc entry is of build {stale}, the library is {build_id}: rejected"
+    return None, "no committed PMC pass for this kernel and size"
+
+
+def valu_issue_peak(pmc):
+    """Architectural VALU issue peak (wave-instructions / cycle / SIMD) for the kernel's measured
+    instruction mix: f64 + conversions at 4 cycles, everything else at 2."""
+    mix = pmc.get("valu_mix")
+    total = float(pmc["valu_instr_per_launch"])
+    if mix:
+        slow = float(mix["f64"]) + float(mix["cvt"])
+        source = pmc.get("valu_mix_source", "PMC")
+    else:   # DESIGN.md section 5 mix of k_episode: 58 f64 + 10 cvt of 114 per inner step
+        slow = total * 68.0 / 114.0
+        source = "DESIGN.md static mix (no PMC mix counters in the entry)"
+    slow = min(slow, total)
+    cyc = (ISSUE_F64_CYCLES * slow + ISSUE_F32_CYCLES * (total - slow)) / total
+    return 1.0 / cyc, cyc, slow / total, source
 
 
 def episode_bytes_per_env(env):
@@ -250,50 +283,74 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         elapsed = shard.max_over_ranks(elapsed, coll_dev)
         inner = shard.sum_over_ranks(inner_local, coll_dev)
         assert all_ret.numel() == N * world
+        shards = shard.gather_ints([lo, lo + N, inner_local], coll_dev)
     else:
         inner = inner_local
+        shards = [[lo, lo + N, inner_local]]
     return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
+                shards=shards,
                 launch="hip graph of the K steps" if graph is not None else "eager")
 
 
-def roofline(env_id, env, N, kern_ms, inner_local, K, simds):
+def roofline(env_id, env, N, kern_ms, inner_local, K, simds, build_id):
     """Roofline of the episode kernel.  Its state stays in registers for all T substeps, so the
     binding resource is VALU instruction issue: achieved = VALU wave-instructions per SIMD per
     clock over the kernel time (instruction count from the committed rocprofv3 PMC pass of this
-    kernel and size), peak = the measured multi-wave issue floor.  HBM is reported beside it."""
+    kernel, size and library build), peak = the architectural issue rate for the kernel's PMC
+    instruction mix (valu_issue_peak).  HBM is reported beside it."""
     kernel = env.episode_kernel()
     bpe = episode_bytes_per_env(env)
     hbm_gbs = bpe * N / (kern_ms * 1e-3) / 1e9
-    pmc = pmc_entry(env_id, N, kernel)
+    pmc, pmc_note = pmc_entry(env_id, N, kernel, build_id)
     hbm = {"achieved_GBps": hbm_gbs, "peak_GBps": HBM_PEAK_GBS, "frac": hbm_gbs / HBM_PEAK_GBS,
            "algorithmic_bytes_per_env": bpe, "algorithmic_bytes_per_launch": bpe * N,
            "bytes_per_inner_step": bpe * N / max(1, inner_local / K)}
-    out = {"kernel": kernel, "kernel_ms": kern_ms, "hbm": hbm}
+    out = {"kernel": kernel, "kernel_ms": kern_ms, "build_id": build_id, "pmc_note": pmc_note, "hbm": hbm}
     if pmc is not None:
         cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
         achieved = pmc["valu_instr_per_launch"] / simds / cyc
-        peak = 1.0 / ISSUE_SIMD_CYCLES
+        peak, peak_cyc, slow_frac, mix_source = valu_issue_peak(pmc)
         traffic = pmc.get("traffic_bytes_per_launch")
         hbm["traffic_over_algorithmic"] = traffic / (bpe * N) if traffic else None
         out.update({"bound": "valu_issue", "achieved": achieved, "peak": peak,
                     "unit": "VALU wave-instr/cycle/SIMD", "frac": achieved / peak, "traffic": traffic,
-                    "peak_note": f"peak = 1/{ISSUE_SIMD_CYCLES} (measured >=4-wave f64 issue floor; the "
-                                 f"architectural 1/{ISSUE_ARCH_CYCLES:g} gives frac "
-                                 f"{achieved * ISSUE_ARCH_CYCLES:.3f}; a lone wave sustains 1/"
-                                 f"{ISSUE_SINGLE_WAVE_CYCLES})",
+                    "peak_note": f"peak = 1/{peak_cyc:.3f}: f64 + cvt ({slow_frac:.3f} of the VALU instructions, "
+                                 f"{mix_source}) at {ISSUE_F64_CYCLES:g} cycles, the rest at {ISSUE_F32_CYCLES:g} "
+                                 f"(MI355X_MICROARCH.md); clock {CLOCK_GHZ} GHz",
+                    "secondary": {"frac_vs_measured_4wave_floor": achieved * ISSUE_SIMD_CYCLES,
+                                  "frac_vs_lone_wave_floor": achieved * ISSUE_SINGLE_WAVE_CYCLES,
+                                  "floors_source": "tools/valu_rates.hip, profiles/r01_valu_rates.jsonl"},
                     "pmc": {k: pmc.get(k) for k in ("valu_instr_per_launch", "valu_instr_per_inner_step_per_env",
-                                                    "valu_busy_pct", "waves", "kernel_ns_median_under_pmc",
-                                                    "build_id", "source")}})
-    else:   # no PMC pass of this kernel / size committed: the HBM roofline alone
+                                                    "valu_mix", "valu_busy_pct", "waves",
+                                                    "kernel_ns_median_under_pmc", "build_id", "source")}})
+    else:   # no PMC pass of this kernel / size / build committed: the HBM roofline alone
         out.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm_gbs / HBM_PEAK_GBS, "traffic": None,
-                    "note": "no committed PMC pass for this kernel and size (profiles/pmc_summary.json)"})
+                    "frac": hbm_gbs / HBM_PEAK_GBS, "traffic": None})
     return out
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` outside a torch.distributed launcher: start the N ranks (one process
+    per GPU) with torch.distributed.run as a child of this process -- which has not touched the GPU
+    -- and return their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["FGX_BENCH_SPAWNED"] = "1"
+    print(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a torch.distributed launcher bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--global-envs", type=int, default=GLOBAL_ENVS,
@@ -307,7 +364,12 @@ def main():
                     help="launch the K steps eagerly instead of replaying them as one HIP graph")
     args = ap.parse_args()
 
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # the CPU baseline runs first, before this process touches the GPU (its workers are forked)
@@ -370,7 +432,13 @@ def main():
                        "T": env.T, "launch": r["launch"],
                        "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"
                        + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
-            "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds),
+            "ranks_seen": dist.get_world_size() if dist is not None else 1,
+            "backend": dist.get_backend() if dist is not None else None,
+            "launcher": ("torch.distributed.run" + (" (spawned by bench.py --gpus)" if os.environ.get("FGX_BENCH_SPAWNED")
+                                                     else "")) if launched else "single process",
+            # per rank: [first global env, end, inner env steps in the timed region]
+            "shards": r["shards"],
+            "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds, lib_build_id()),
         }
         if weak is not None:
             line["weak_scaling"] = weak

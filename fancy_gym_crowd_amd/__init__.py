@@ -14,10 +14,11 @@ hand-written HIP kernels (libfgx.so) on the GPU.
 """
 from .registry import (ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS, ENV_SPECS, KNOWN_MPS,  # noqa: F401
                        MOVEMENT_PRIMITIVE_ENVIRONMENTS_FOR_NS, REPLAN_CLOSE, ReplanAny, ReplanAt,
-                       ReplanEvery, ReplanNormPeriod, nested_update, register, resolve, upgrade)
+                       ReplanEvery, ReplanNormPeriod, TrajValidity, nested_update, register, resolve,
+                       upgrade)
 
 __all__ = ["make", "BlackBoxVectorEnv", "StepVectorEnv", "ReplanEvery", "ReplanAt", "ReplanNormPeriod",
-           "ReplanAny", "REPLAN_CLOSE", "register", "upgrade", "resolve",
+           "ReplanAny", "REPLAN_CLOSE", "TrajValidity", "register", "upgrade", "resolve",
            "ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS", "KNOWN_MPS"]
 
 

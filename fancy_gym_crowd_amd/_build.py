@@ -81,10 +81,25 @@ def _deps(path, seen=None):
     return seen
 
 
+_TOOLCHAIN = None
+
+
+def toolchain_id():
+    """`hipcc --version` (compiler and ROCm release): part of every object's cache key, so a
+    toolchain change recompiles."""
+    global _TOOLCHAIN
+    if _TOOLCHAIN is None:
+        try:
+            _TOOLCHAIN = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True).stdout
+        except OSError:
+            _TOOLCHAIN = "unknown"
+    return _TOOLCHAIN
+
+
 def _unit_key(src, bid):
-    """Object cache key of one translation unit: flags, its include closure and (fgx_api.hip only,
-    the unit that embeds it) the library build id."""
-    h = hashlib.sha256(" ".join(FLAGS + UNIT_FLAGS.get(src, [])).encode())
+    """Object cache key of one translation unit: toolchain, flags, its include closure and
+    (fgx_api.hip only, the unit that embeds it) the library build id."""
+    h = hashlib.sha256(toolchain_id().encode() + b"\0" + " ".join(FLAGS + UNIT_FLAGS.get(src, [])).encode())
     if src == "fgx_api.hip":
         h.update(bid.encode())
     for f in sorted(_deps(os.path.join(CSRC, src))):
@@ -94,10 +109,10 @@ def _unit_key(src, bid):
     return h.hexdigest()[:16]
 
 
-def _compile(src, bid, verbose):
+def _compile(src, bid, verbose, force=False):
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
     key = _unit_key(src, bid)
-    if os.path.exists(obj) and os.path.exists(obj + ".key") and open(obj + ".key").read().strip() == key:
+    if not force and os.path.exists(obj) and os.path.exists(obj + ".key") and open(obj + ".key").read().strip() == key:
         return obj   # unchanged unit: reuse its object
     defs = [f'-DFGX_BUILD_ID="{bid}"'] if src == "fgx_api.hip" else []
     cmd = [_hipcc(), *FLAGS, *UNIT_FLAGS.get(src, []), *defs, "-I", INC, "-c", os.path.join(CSRC, src), "-o",
@@ -143,7 +158,7 @@ def build(force=False, verbose=True):
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, bid, verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, bid, verbose, force), SOURCES))   # force: no cached objects
     cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

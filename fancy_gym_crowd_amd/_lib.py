@@ -11,13 +11,15 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 5
+FGX_ABI_VERSION = 6
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
 SCHED_EVERY, SCHED_AT, SCHED_NORM_PERIOD = 0, 1, 2
 MP_NONE, MP_PROMP, MP_DMP, MP_PRODMP = 0, 1, 2, 3
 PHASE_LINEAR, PHASE_EXP = 0, 1
 CTRL_PD, CTRL_VEL, CTRL_POS = 0, 1, 2
+VALID_TAU, VALID_DELAY, VALID_POS = 1, 2, 4
+INVALID_OBS_ZEROS, INVALID_OBS_CURRENT = 0, 1
 ERRORS = {-1: "FGX_E_INVALID", -2: "FGX_E_HIP", -3: "FGX_E_NOMEM", -4: "FGX_E_UNSUPPORTED"}
 
 
@@ -40,7 +42,11 @@ class FgxConfig(ctypes.Structure):
         ("sched_i0", ctypes.c_int32 * 4), ("sched_i1", ctypes.c_int32 * 4),
         ("sched_mul", ctypes.c_double * 4), ("sched_div", ctypes.c_double * 4),
         ("n_gains", ctypes.c_int32), ("reserved1", ctypes.c_int32),
-        ("p_gains", ctypes.c_double * 8), ("d_gains", ctypes.c_double * 8)]
+        ("p_gains", ctypes.c_double * 8), ("d_gains", ctypes.c_double * 8)] + [
+        (n, ctypes.c_int32) for n in ("valid_flags", "invalid_obs", "invalid_terminated", "invalid_truncated")] + [
+        (n, ctypes.c_double) for n in ("invalid_reward", "valid_tau_lo", "valid_tau_hi", "valid_delay_lo",
+                                       "valid_delay_hi")] + [
+        ("valid_pos_lo", ctypes.c_double * 8), ("valid_pos_hi", ctypes.c_double * 8)]
 
 
 class FgxDims(ctypes.Structure):

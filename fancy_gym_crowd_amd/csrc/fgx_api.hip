@@ -151,7 +151,9 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
       return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14
-    if (!(c.tau > 0.0) || !(c.dt > 0.0)) return fail(FGX_E_INVALID, "tau/dt must be positive");
+    if (!(c.tau > 0.0) || !(c.dt > 0.0) || !std::isfinite(c.tau)) return fail(FGX_E_INVALID, "tau/dt must be positive");
+    // a negative delay would look up basis rows after the current one (prodmp_delay_index)
+    if (!(c.delay >= 0.0) || !std::isfinite(c.delay)) return fail(FGX_E_INVALID, "delay must be finite and >= 0");
   }
   if (c.time_aware && c.return_context) return fail(FGX_E_INVALID, "time_aware with context observation");
   std::memset(&d, 0, sizeof(d));
@@ -276,6 +278,21 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.gs32 = (float)c.goal_scale;
   d.alpha32 = (float)c.alpha;
   d.beta32 = (float)(c.alpha / 4);
+  // trajectory validity (raw_interface_wrapper.py:55-72,103-121)
+  if (c.valid_flags & ~(FGX_VALID_TAU | FGX_VALID_DELAY | FGX_VALID_POS)) return fail(FGX_E_INVALID, "bad valid_flags");
+  if (c.valid_flags && c.mp_kind == FGX_MP_NONE) return fail(FGX_E_INVALID, "trajectory validity needs a movement primitive");
+  if ((c.valid_flags & FGX_VALID_TAU) && !c.learn_tau) return fail(FGX_E_INVALID, "FGX_VALID_TAU needs learn_tau");
+  if ((c.valid_flags & FGX_VALID_DELAY) && !c.learn_delay) return fail(FGX_E_INVALID, "FGX_VALID_DELAY needs learn_delay");
+  if (c.invalid_obs != FGX_INVALID_OBS_ZEROS && c.invalid_obs != FGX_INVALID_OBS_CURRENT)
+    return fail(FGX_E_INVALID, "bad invalid_obs");
+  d.valid_flags = c.valid_flags;
+  d.invalid_obs = c.invalid_obs;
+  d.invalid_term = c.invalid_terminated != 0;
+  d.invalid_trunc = c.invalid_truncated != 0;
+  d.invalid_reward = c.invalid_reward;
+  d.vtau_lo32 = (float)c.valid_tau_lo; d.vtau_hi32 = (float)c.valid_tau_hi;
+  d.vdelay_lo32 = (float)c.valid_delay_lo; d.vdelay_hi32 = (float)c.valid_delay_hi;
+  for (int k = 0; k < kMaxLinks; ++k) { d.vpos_lo[k] = c.valid_pos_lo[k]; d.vpos_hi[k] = c.valid_pos_hi[k]; }
   return FGX_OK;
 }
 
@@ -395,6 +412,22 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   if (rc) { fgx_destroy(h); return rc; }
   e = hipDeviceSynchronize();
   if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("create sync: ") + hipGetErrorString(e)); }
+  // NaN-free guard bound of the ProMP fast blocks: the largest row L1 norm of the basis columns
+  h->dc.wbound32 = 1e30f;
+  if (d.mp == MP_PROMP && d.rows > 0) {
+    const size_t n = (size_t)d.rows * d.stride;
+    float* ht = new float[n];
+    e = hipMemcpy(ht, h->tables, n * sizeof(float), hipMemcpyDeviceToHost);
+    double l1max = 0.0;
+    for (int i = 0; e == hipSuccess && i < d.rows; ++i) {
+      double l1 = 0.0;
+      for (int j = 0; j < d.nb; ++j) l1 += std::fabs((double)ht[(size_t)i * d.stride + j]);
+      l1max = std::isnan(l1) ? INFINITY : (l1 > l1max ? l1 : l1max);
+    }
+    delete[] ht;
+    if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, "hipMemcpy tables"); }
+    h->dc.wbound32 = l1max > 1.0 ? (float)(1e30 / l1max) : 1e30f;   // (inf table: 0, every wave exact)
+  }
   *handle = h;
   return FGX_OK;
 }
@@ -498,7 +531,8 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
     hh.st.plan_len = h->plan_len;
     o.positions = nullptr;
     o.velocities = nullptr;
-    return launch_episode(hh, MP_GIVEN, nullptr, P, V, o, (hipStream_t)stream);
+    // (params only for the validity checks of the raw tau / delay entries)
+    return launch_episode(hh, MP_GIVEN, params, P, V, o, (hipStream_t)stream);
   }
   return launch_episode(*h, h->dc.mp, params, nullptr, nullptr, o, (hipStream_t)stream);
 }
@@ -585,7 +619,8 @@ int fgx_episode_kernel(void* handle, int32_t info_level) {
   Handle* h = (Handle*)handle;
   if (!h) return fail(FGX_E_INVALID, "null handle");
   const int mp = h->learned() ? MP_GIVEN : h->dc.mp;
-  return episode_kernel_choice(h->dc, mp, info_level >= 2, h->learned());
+  // the predicate launch_episode_nl uses: any per-step output, or the validity checks
+  return episode_kernel_choice(h->dc, mp, info_level >= 1 || h->dc.valid_flags != 0, h->learned());
 }
 
 }  // extern "C"

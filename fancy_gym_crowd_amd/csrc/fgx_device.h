@@ -28,6 +28,7 @@ enum : int { REW_SIMPLE = 0, REW_VEL_ACC = 1, REW_UNBOUNDED = 2 };
 enum : int { SCHED_EVERY = 0, SCHED_AT = 1, SCHED_NORM_PERIOD = 2 };
 enum : int { MP_NONE = 0, MP_PROMP = 1, MP_DMP = 2, MP_PRODMP = 3, MP_GIVEN = 4 };
 enum : int { CTRL_PD = 0, CTRL_VEL = 1, CTRL_POS = 2 };
+enum : int { VALID_TAU = 1, VALID_DELAY = 2, VALID_POS = 4, INVALID_OBS_ZEROS = 0, INVALID_OBS_CURRENT = 1 };
 
 // Table layouts (row = absolute env step index i, see oracle/mp.py):
 //   ProMP : [phi_0 .. phi_{nb-1}, dt32]                      stride nb + 1
@@ -62,6 +63,14 @@ struct DevCfg {
   double delay, alpha_phase, bandwidth;   // phase / basis generator (per-env tables)
   float tau_lo32, tau_hi32, delay_lo32, delay_hi32;   // action-space bounds of tau / delay
   float ws32, gs32, alpha32, beta32;
+  // trajectory validity (include/fgx.h FGX_VALID_*; only the logging k_episode reads these)
+  int valid_flags, invalid_obs, invalid_term, invalid_trunc;
+  float vtau_lo32, vtau_hi32, vdelay_lo32, vdelay_hi32;
+  double invalid_reward;
+  double vpos_lo[kMaxLinks], vpos_hi[kMaxLinks];
+  // ProMP NaN-free wave guard (k_episode / k_episode_jl fast blocks): every |w| < wbound32 bounds
+  // |pos| <= max_i sum_j |table_ij| |w_j| < 1e30 (the table carries weights_scale); set by fgx_create
+  float wbound32;
 };
 
 // SoA env state, owned by the handle ([k][N] for per-link arrays).

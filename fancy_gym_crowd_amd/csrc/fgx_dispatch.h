@@ -135,8 +135,9 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
   const int threads = 256;
   const int blocks = (int)((c.N + threads - 1) / threads);
   const size_t lds = (MP == MP_GIVEN) ? 0 : (size_t)c.rows * c.stride * sizeof(float);
+  // the logging instantiation also runs the trajectory-validity checks (c.valid_flags)
   const bool log = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided ||
-                   o.end_effector || o.reward_dist;
+                   o.end_effector || o.reward_dist || c.valid_flags != 0;
   if constexpr (MP != MP_GIVEN && NB != 0) {
     if (c.stride != Traj<MP, 1, NB>::KS) {
       err = "basis table stride does not match the compiled layout";

@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
       for (int j = 0; j < 8; ++j) { P[j] = Pn[j]; V[j] = Vn[j]; }
     }
   };
-  // ProMP NaN-free waves (k_episode's guard): with |w| < 1e30 and |q|, |qd|, |p|, |d| < 1e150 every
+  // ProMP NaN-free waves (k_episode's guard): with |w| < c.wbound32 and |q|, |qd|, |p|, |d| < 1e150 every
   // PD control u of the plan is finite, so np.clip's NaN propagation never applies
   bool nan_free = true;
   if constexpr (PKT) {
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
               __builtin_fabs(q) < 1e150 && __builtin_fabs(qd) < 1e150 && __builtin_fabs(pg) < 1e150 &&
               __builtin_fabs(dg) < 1e150;
 #pragma unroll
-    for (int j = 0; j < NBL; ++j) ok = ok && __builtin_fabsf(tg.w[0][j]) < 1e30f;
+    for (int j = 0; j < NBL; ++j) ok = ok && __builtin_fabsf(tg.w[0][j]) < c.wbound32;
     nan_free = __ballot(valid && !ok) == 0;
   }
 

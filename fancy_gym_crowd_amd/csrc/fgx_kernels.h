@@ -641,6 +641,71 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   s.plans[e] = plans;
 }
 
+// ============================================================================ trajectory validity
+// RawInterfaceWrapper.preprocessing_and_validity_callback (raw_interface_wrapper.py:55-72) as the
+// checks of include/fgx.h FGX_VALID_* (the form of table_tennis_env.py:304-309): the raw learned
+// tau / delay entries against their bounds (f32 compares: a float32 action entry against a Python
+// float), the desired positions of the whole plan against per-joint bounds (f64 compares of the f32
+// positions).  tg: a copy of the plan's generator (advanced here); dpos: caller-given plan.
+template <int MP, int NL, typename TrajT>
+__device__ inline bool plan_valid(const DevCfg& c, TrajT tg, const float* prow, const float* dpos, int64_t e, int Te) {
+  if (prow && (c.valid_flags & VALID_TAU)) {
+    const float t = prow[0];
+    if (t > c.vtau_hi32 || t < c.vtau_lo32) return false;
+  }
+  if (prow && (c.valid_flags & VALID_DELAY)) {
+    const float dl = prow[c.learn_tau ? 1 : 0];
+    if (dl > c.vdelay_hi32 || dl < c.vdelay_lo32) return false;
+  }
+  if (c.valid_flags & VALID_POS) {
+    float pos[NL], vel[NL];
+    for (int k = 0; k < Te; ++k) {
+      if constexpr (MP == MP_GIVEN) {
+#pragma unroll
+        for (int d = 0; d < NL; ++d) pos[d] = dpos[(e * c.T + k) * NL + d];
+      } else {
+        tg.at(c, k, pos, vel);
+      }
+#pragma unroll
+      for (int d = 0; d < NL; ++d)
+        if ((double)pos[d] > c.vpos_hi[d] || (double)pos[d] < c.vpos_lo[d]) return false;
+    }
+  }
+  return true;
+}
+
+// invalid_traj_callback's artificial transition (raw_interface_wrapper.py:103-121,
+// black_box_wrapper.py:194-197): no env step, no plan counted; return / flags from the config, the
+// observation zeros (np.zeros, the reference default) or the env's current one; then the VectorEnv
+// auto-reset when the artificial flags end the episode.
+template <int NL>
+__device__ inline void invalid_transition(const DevCfg& c, const DevState& s, const Outputs& o, int64_t e, Env<NL>& v) {
+  o.ret[e] = c.invalid_reward;
+  o.term[e] = c.invalid_term;
+  o.trunc[e] = c.invalid_trunc;
+  o.tlen[e] = 0;
+  v.fk();
+  float* ob = o.obs + e * c.out_dim;
+  float* fo = o.final_obs ? o.final_obs + e * c.out_dim : nullptr;
+  auto artificial = [&](float* d) {
+    if (!d) return;
+    if (c.invalid_obs == INVALID_OBS_CURRENT) emit_obs(c, v, c.return_context, d, nullptr);
+    else
+      for (int i = 0; i < c.out_dim; ++i) d[i] = 0.0f;
+  };
+  if (o.autoreset && (c.invalid_term || c.invalid_trunc)) {
+    artificial(fo);
+    autoreset_env(c, s, e, v);
+    v.flags = 0;
+    emit_obs(c, v, c.return_context, ob, nullptr, true);
+    store_env(c, s, e, v, c.env != ENV_SIMPLE);
+    s.plans[e] = 0;
+  } else {   // the env state and plan count are unchanged
+    artificial(ob);
+    artificial(fo);
+  }
+}
+
 // ============================================================================ the BB step
 // The body of k_episode (below) and k_episode_w2 (the same code compiled for two resident waves
 // per SIMD).
@@ -688,6 +753,36 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   // replanning sample) and the two-level online sum is exact; the direct envs can stop at any
   // sample (collision) and keep their step rewards in s.rew for lengths above 128.
   const int Te = (MP == MP_GIVEN && s.plan_len) ? s.plan_len[e] : c.T;
+  // the per-step info rows L..T-1: the full desired plan (black_box_wrapper.py:245-246), NaN (0 for
+  // the flags) in the per-step arrays after trajectory_length; gen: the plan's generator at sample L
+  auto pad_info = [&](int L, auto& gen) {
+    const double dnan = __builtin_nan("");
+    const float fnan = __builtin_nanf("");
+    float pp[NL], pv[NL];
+    for (int kk = L; kk < c.T; ++kk) {
+      const int64_t ek = (int64_t)kk * N + e;
+      if (o.positions && MP != MP_GIVEN) {
+        gen.at(c, kk, pp, pv);
+        for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pp[d]; o.velocities[ek * NL + d] = pv[d]; }
+      }
+      if (o.step_actions)
+        for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = dnan;
+      if (o.step_rewards) o.step_rewards[ek] = dnan;
+      if (o.step_obs)
+        for (int q = 0; q < c.full_dim; ++q) o.step_obs[ek * c.full_dim + q] = fnan;
+      if (o.is_collided) { o.is_collided[ek] = 0; o.is_success[ek] = 0; }
+      if (o.end_effector) { o.end_effector[ek * 2] = dnan; o.end_effector[ek * 2 + 1] = dnan; }
+      if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
+    }
+  };
+  if constexpr (LOG) {   // trajectory validity (the logging instantiation serves valid_flags != 0)
+    if (c.valid_flags &&
+        !plan_valid<MP, NL>(c, tg, params ? params + e * c.n_params : nullptr, dpos, e, Te)) {
+      pad_info(0, tg);
+      invalid_transition(c, s, o, e, v);
+      return;
+    }
+  }
   int split = 0;
   if (ENV == ENV_SIMPLE && !c.sched_state) {
     int Lp = min(Te, max(1, c.max_steps - v.steps));
@@ -953,8 +1048,9 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     bool fast_ok = __ballot(1) == ~0ull;   // partial wave (N % 64 != 0): generic path only
     if (MP == MP_PROMP && CTRL == CTRL_PD) {
       // NaN-free waves: the PD control u = p (pos - q) + d (vel - qd) is finite for every sample
-      // of the plan when, for every lane, |w| < 1e30 and |q|, |qd|, |p|, |d| < 1e150:
-      //   |pos| <= sum_j phi_j |w_j| < 1e30 (normalised basis), |vel| <= 2 |pos| / dt < 2e32
+      // of the plan when, for every lane, |w| < c.wbound32 and |q|, |qd|, |p|, |d| < 1e150:
+      //   |pos| <= max_i sum_j |table_ij| |w_j| < 1e30 (wbound32 = 1e30 / max(1, the table's largest
+      //   row L1 norm), which carries weights_scale, fgx_create), |vel| <= 2 |pos| / dt < 2e32
       //   (finite in f32); the clipped |a| <= act_hi = 1000 bounds 200 Euler steps to
       //   |qd| < 1e150 + 2e3, |q| < 3.1e150, so |p (pos - q)|, |d (vel - qd)| < 4e300 and their
       //   sum < 8e300 < DBL_MAX: no inf - inf, no 0 * inf, no overflow.
@@ -965,7 +1061,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
         ok = ok && __builtin_fabs(v.q[d]) < 1e150 && __builtin_fabs(v.qd[d]) < 1e150 &&
              __builtin_fabs(c.pg[d]) < 1e150 && __builtin_fabs(c.dg[d]) < 1e150;
 #pragma unroll
-        for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.wt(d, j)) < 1e30f;
+        for (int j = 0; j < (NB ? NB : kGenBasis); ++j) ok = ok && __builtin_fabsf(tg.wt(d, j)) < c.wbound32;
       }
       if (__ballot(!ok) != 0) fast_ok = false;
     }
@@ -1033,27 +1129,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   }
   FGX_STAMP(o, e, 3);
   const int L = k;   // samples executed (trajectory_length)
-  if (LOG) {
-    // the full desired plan is reported (black_box_wrapper.py:245-246); the per-step arrays end
-    // at trajectory_length: rows L..T-1 are padded with NaN (0 for the flags) in the same pass
-    const double dnan = __builtin_nan("");
-    const float fnan = __builtin_nanf("");
-    for (int kk = L; kk < c.T; ++kk) {
-      const int64_t ek = (int64_t)kk * N + e;
-      if (o.positions && MP != MP_GIVEN) {
-        tg.at(c, kk, pos, vel);
-        for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
-      }
-      if (o.step_actions)
-        for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = dnan;
-      if (o.step_rewards) o.step_rewards[ek] = dnan;
-      if (o.step_obs)
-        for (int q = 0; q < c.full_dim; ++q) o.step_obs[ek * c.full_dim + q] = fnan;
-      if (o.is_collided) { o.is_collided[ek] = 0; o.is_success[ek] = 0; }
-      if (o.end_effector) { o.end_effector[ek * 2] = dnan; o.end_effector[ek * 2 + 1] = dnan; }
-      if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
-    }
-  }
+  if (LOG) pad_info(L, tg);
   // the epilogue needs FK of the final q; a last sample at env step >= 199 (always a generic one)
   // has just computed it for its reward
   if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();

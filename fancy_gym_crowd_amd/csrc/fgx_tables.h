@@ -118,8 +118,12 @@ __device__ inline void prodmp_row(const DevCfg& c, double s, const double* p1, c
 // initial position and velocity there (test_black_box.py:267-307).  j(i) <= i, non-decreasing.
 __device__ inline int prodmp_delay_index(const DevCfg& c, int i, double tau, double delay) {
   double u = ((double)i * c.dt - delay) / tau;
-  u = u > 0.0 ? u : 0.0;
-  return (int)rint(u / (c.dt / tau));
+  u = u > 0.0 ? u : 0.0;                       // (NaN -> 0)
+  // j <= i holds for every delay >= 0 (fgx_create refuses a negative or non-finite static delay,
+  // learned delays are clipped to delay_bound, lo >= 0); the clamp keeps any other value inside
+  // the rows already computed
+  const double j = rint(u / (c.dt / tau));
+  return j < (double)i ? (int)j : i;
 }
 
 // One env's ProDMP rows 0..R-1 for its own tau, sequentially in one thread (the cumulative

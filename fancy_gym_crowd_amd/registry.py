@@ -58,8 +58,9 @@ _MP_PYTORCH_DEFAULTS = dict(alpha_phase=3.0, delay=0.0, basis_bandwidth_factor=3
 class EnvSpec:
     """A registered step-based env (what gym.make('fancy/<Name>-v0') builds)."""
 
-    def __init__(self, id, kind, kwargs, max_episode_steps, mp_config):
+    def __init__(self, id, kind, kwargs, max_episode_steps, mp_config, traj_validity=None):
         self.id = id
+        self.traj_validity = traj_validity    # TrajValidity (the MPWrapper's validity hooks) or None
         self.kind = kind                      # 'simple' (torque) | 'hole' | 'via' (direct velocity)
         self.kwargs = dict(kwargs)
         self.max_episode_steps = max_episode_steps
@@ -105,9 +106,10 @@ def nested_update(base, update):
 
 
 def register(id, kind, kwargs, max_episode_steps=200, mp_config=None, add_mp_types=KNOWN_MPS,
-             mp_config_override=None):
-    """Register a step-based reacher id and its '{ns}_{MP}/{name}' black-box ids (registry.py:137-183)."""
-    spec = EnvSpec(id, kind, kwargs, max_episode_steps, mp_config or {})
+             mp_config_override=None, traj_validity=None):
+    """Register a step-based reacher id and its '{ns}_{MP}/{name}' black-box ids (registry.py:137-183).
+    traj_validity: TrajValidity, the variant's MPWrapper validity hooks (default: every plan valid)."""
+    spec = EnvSpec(id, kind, kwargs, max_episode_steps, mp_config or {}, traj_validity)
     ENV_SPECS[id] = spec
     upgrade(id, add_mp_types=add_mp_types, mp_config_override=mp_config_override)
     return spec
@@ -291,6 +293,75 @@ def _schedule_period(schedule, max_steps):
     raise NotImplementedError("not a t % k == 0 schedule")
 
 
+# --------------------------------------------------------------------------- trajectory validity
+class TrajValidity:
+    """The env-side validity hooks of a black-box env, run on the device (include/fgx.h FGX_VALID_*):
+    RawInterfaceWrapper.preprocessing_and_validity_callback / invalid_traj_callback
+    (raw_interface_wrapper.py:55-72,103-121, called at black_box_wrapper.py:178-197).  The registered
+    reachers keep the reference's identity default (every plan valid); a registered variant or a
+    make() call passes ``traj_validity=TrajValidity(...)`` for the checks the reference's overriding
+    envs make (table_tennis_env.py:304-309):
+
+      tau=(lo, hi)        raw learned tau action[0] inside [lo, hi]          (needs learn_tau)
+      delay=(lo, hi)      raw learned delay action[learn_tau] inside [lo, hi] (needs learn_delay)
+      pos_low / pos_high  per-joint bounds on the desired positions of the whole plan
+
+    An invalid plan yields the artificial transition (no env step, trajectory_length 0):
+    return ``invalid_return``, ``terminated`` / ``truncated`` as given (reference default: True /
+    False), observation zeros (``obs='zeros'``, np.zeros) or the env's current one
+    (``obs='current'``).  ``__call__`` is the host predicate with the reference's signature."""
+
+    def __init__(self, tau=None, delay=None, pos_low=None, pos_high=None, invalid_return=0.0,
+                 terminated=True, truncated=False, obs='zeros'):
+        if obs not in ('zeros', 'current'):
+            raise ValueError("obs must be 'zeros' or 'current'")
+        if (pos_low is None) != (pos_high is None):
+            raise ValueError("pos_low and pos_high go together")
+        self.tau = None if tau is None else (float(tau[0]), float(tau[1]))
+        self.delay = None if delay is None else (float(delay[0]), float(delay[1]))
+        self.pos_low = None if pos_low is None else np.asarray(pos_low, np.float64).reshape(-1)
+        self.pos_high = None if pos_high is None else np.asarray(pos_high, np.float64).reshape(-1)
+        self.invalid_return = float(invalid_return)
+        self.terminated, self.truncated, self.obs = bool(terminated), bool(truncated), obs
+
+    def __call__(self, action, pos_traj, vel_traj, tau_bound=None, delay_bound=None, learn_tau=True):
+        """(valid, pos_traj, vel_traj) for one env, as preprocessing_and_validity_callback."""
+        a = np.asarray(action, np.float32)
+        if self.tau is not None and (a[0] > self.tau[1] or a[0] < self.tau[0]):
+            return False, pos_traj, vel_traj
+        i = 1 if learn_tau else 0
+        if self.delay is not None and (a[i] > self.delay[1] or a[i] < self.delay[0]):
+            return False, pos_traj, vel_traj
+        if self.pos_low is not None and (np.any(pos_traj > self.pos_high) or np.any(pos_traj < self.pos_low)):
+            return False, pos_traj, vel_traj
+        return True, pos_traj, vel_traj
+
+    def encode(self, c, n_links):
+        flags = 0
+        if self.tau is not None:
+            if not c.learn_tau:
+                raise ValueError("TrajValidity(tau=...) needs learn_tau")
+            flags |= _lib.VALID_TAU
+            c.valid_tau_lo, c.valid_tau_hi = self.tau
+        if self.delay is not None:
+            if not c.learn_delay:
+                raise ValueError("TrajValidity(delay=...) needs learn_delay")
+            flags |= _lib.VALID_DELAY
+            c.valid_delay_lo, c.valid_delay_hi = self.delay
+        if self.pos_low is not None:
+            lo = np.broadcast_to(self.pos_low, (n_links,)) if self.pos_low.size in (1, n_links) else self.pos_low
+            hi = np.broadcast_to(self.pos_high, (n_links,)) if self.pos_high.size in (1, n_links) else self.pos_high
+            if lo.shape != (n_links,) or hi.shape != (n_links,):
+                raise ValueError(f"pos_low / pos_high need {n_links} entries")
+            flags |= _lib.VALID_POS
+            for k in range(n_links):
+                c.valid_pos_lo[k], c.valid_pos_hi[k] = float(lo[k]), float(hi[k])
+        c.valid_flags = flags
+        c.invalid_reward = self.invalid_return
+        c.invalid_terminated, c.invalid_truncated = int(self.terminated), int(self.truncated)
+        c.invalid_obs = _lib.INVALID_OBS_CURRENT if self.obs == 'current' else _lib.INVALID_OBS_ZEROS
+
+
 # --------------------------------------------------------------------------- resolution
 def parse_id(env_id):
     ns_mp, _, name = env_id.partition('/')
@@ -308,6 +379,9 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     spec = ENV_SPECS[base_id]
     kw = dict(spec.kwargs)
     kw.update(env_kwargs)
+    validity = kw.pop('traj_validity', spec.traj_validity)
+    if validity is not None and not isinstance(validity, TrajValidity):
+        raise ValueError("traj_validity must be a fgx.TrajValidity")
     c = _lib.FgxConfig()
     c.abi_version = _lib.FGX_ABI_VERSION
     n = int(kw['n_links'])
@@ -486,4 +560,7 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     else:
         raise ValueError("reward_aggregation must be callable")
     meta['n_params'] = n * c.n_basis + (0 if tg_type == 'promp' else n) + int(learn_tau) + int(learn_delay)
+    if validity is not None:
+        validity.encode(c, n)
+    meta['traj_validity'] = validity
     return c, meta

@@ -48,3 +48,12 @@ def sum_over_ranks(x, device, group=None):
     t = torch.tensor([int(x)], dtype=torch.int64, device=device)
     dist.all_reduce(t, group=group)
     return int(t.item())
+
+
+def gather_ints(values, device, group=None):
+    """all_gather a short list of ints from every rank -> [world][len(values)] (rank order)."""
+    import torch.distributed as dist
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [[int(x) for x in p.tolist()] for p in parts]

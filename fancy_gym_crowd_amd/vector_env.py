@@ -205,11 +205,16 @@ class BlackBoxVectorEnv:
         _reset_engine(self, seed, options, obs)
         return obs, {}
 
+    def _needs_step_rewards(self):
+        """A reward_aggregation other than sum / mean reads the per-step rewards."""
+        return self.meta["reward_aggregation"] not in ("sum", "mean")
+
     def _info_buffers(self):
         """Per-step info arrays of the info level (module docstring).  The device writes them
         time-major ([T, N, ...], coalesced across envs, include/fgx.h fgx_info); the caller sees
-        [N, T, ...] transposed views.  A generic reward_aggregation also needs step_rewards."""
-        generic_agg = callable(self.meta["reward_aggregation"])
+        [N, T, ...] transposed views.  A reward_aggregation other than sum / mean also needs
+        step_rewards."""
+        generic_agg = self._needs_step_rewards()
         if self.info_level == 0 and not generic_agg:
             return None, {}
         N, T, n, dev = self.num_envs, self.T, self.dof, self.device
@@ -296,14 +301,19 @@ class BlackBoxVectorEnv:
         term, trunc = te.bool(), tr.bool()
         agg = self.meta["reward_aggregation"]
         if agg == "mean":
-            ret = ret / tl.to(torch.float64)
-        elif callable(agg):   # any callable on rewards[:t+1] (black_box_wrapper.py:252), host numpy
+            ret = torch.where(tl > 0, ret / tl.to(torch.float64), ret)   # (tl 0: an invalid plan's return)
+        elif agg in _DEVICE_AGG:   # np.max / np.min / np.median of rewards[:t+1] on the device
+            ret = torch.where(tl > 0, _DEVICE_AGG[agg](bufs["step_rewards"], tl), ret)
+        elif callable(agg):
+            # any other callable on rewards[:t+1] (black_box_wrapper.py:252): user Python, applied
+            # per env on the host -- a device sync and O(N) interpreter work per step
             rew = bufs["step_rewards"].detach().cpu().numpy()
             L = tl.detach().cpu().numpy()
-            ret = torch.tensor([float(agg(rew[i, :L[i]])) for i in range(self.num_envs)], dtype=torch.float64,
-                               device=self.device)
-            if self.info_level < 2:
-                bufs = {k: v for k, v in bufs.items() if k != "step_rewards"}
+            r0 = ret.detach().cpu().numpy()
+            ret = torch.tensor([float(agg(rew[i, :L[i]])) if L[i] > 0 else float(r0[i]) for i in range(self.num_envs)],
+                               dtype=torch.float64, device=self.device)
+        if agg not in ("sum", "mean") and self.info_level < 2:
+            bufs = {k: v for k, v in bufs.items() if k != "step_rewards"}
         per_env = {"trajectory_length": tl}
         per_env.update(bufs)
         info = dict(per_env)
@@ -370,8 +380,12 @@ class BlackBoxVectorEnv:
 
     def episode_kernel(self, info_level=None):
         """Name of the HIP kernel step() launches (fgx_episode_kernel): k_episode, k_episode_jp,
-        k_episode_ws, k_episode_jl or k_episode_w2; all five produce bit-identical results."""
+        k_episode_ws, k_episode_jl or k_episode_w2; all five produce bit-identical results.  The
+        launch takes the logging k_episode whenever some per-step array is written: info_level >= 1,
+        or a reward_aggregation that reads step_rewards."""
         lvl = self.info_level if info_level is None else int(info_level)
+        if self._needs_step_rewards():
+            lvl = max(lvl, 1)
         k = self._eng.lib.fgx_episode_kernel(self._eng.h, lvl)
         if k < 0:
             _lib.check(k)
@@ -437,6 +451,39 @@ class StepVectorEnv:
 
     def close(self):
         self._eng.close()
+
+
+def _masked_rows(step_rewards, tl, fill):
+    """[N, T] view of the time-major rewards with the samples at or after trajectory_length set to
+    `fill` (the kernel writes NaN there)."""
+    T = step_rewards.shape[1]
+    valid = torch.arange(T, device=step_rewards.device)[None, :] < tl.to(torch.int64)[:, None]
+    return torch.where(valid, step_rewards, torch.full_like(step_rewards, fill)), valid
+
+
+def _agg_max(step_rewards, tl):
+    return _masked_rows(step_rewards, tl, -np.inf)[0].amax(dim=1)   # NaN propagates as in np.max
+
+
+def _agg_min(step_rewards, tl):
+    return _masked_rows(step_rewards, tl, np.inf)[0].amin(dim=1)
+
+
+def _agg_median(step_rewards, tl):
+    """np.median of rewards[:L] per row: the mean of the two middle order statistics ((a + b) / 2,
+    or a / 1 for odd L -- numpy's mean of the partitioned middle), NaN if any reward is NaN."""
+    x, valid = _masked_rows(step_rewards, tl, np.inf)
+    has_nan = (torch.isnan(step_rewards) & valid).any(dim=1)
+    xs = torch.sort(torch.nan_to_num(x, nan=np.inf), dim=1).values   # pads (+inf) sort after the samples
+    L = tl.to(torch.int64).clamp(min=1)
+    lo = xs.gather(1, ((L - 1) // 2)[:, None])[:, 0]
+    hi = xs.gather(1, (L // 2)[:, None])[:, 0]
+    med = torch.where(L % 2 == 1, lo, (lo + hi) / 2.0)
+    return torch.where(has_nan, torch.full_like(med, np.nan), med)
+
+
+# reductions of rewards[:t+1] run on the device (black_box_wrapper.py:252)
+_DEVICE_AGG = {np.max: _agg_max, np.amax: _agg_max, np.min: _agg_min, np.amin: _agg_min, np.median: _agg_median}
 
 
 def _reset_engine(env, seed, options, obs):

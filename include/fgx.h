@@ -11,7 +11,7 @@
  *   fgx_reset         BlackBoxWrapper.reset -> env.reset(seed)          black_box/black_box_wrapper.py:258-267,
  *                                                                       base_reacher/base_reacher.py:73-93,
  *                                                                       simple_reacher/simple_reacher.py:46-54,
- *                                                                       hole_reacher/hole_reacher.py:242-253
+ *                                                                       hole_reacher/hole_reacher.py:60-112
  *   fgx_step          BlackBoxWrapper.step(action) (+ VectorEnv         black_box/black_box_wrapper.py:170-253
  *                     autoreset)                                        (gymnasium SyncVectorEnv.step [EXT-M])
  *   fgx_step_traj     BlackBoxWrapper.step with the desired trajectory  black_box/black_box_wrapper.py:177-253
@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 5
+#define FGX_ABI_VERSION 6
 
 /* error codes */
 #define FGX_OK 0
@@ -72,6 +72,22 @@ extern "C" {
 #define FGX_REW_SIMPLE 0     /* hr_simple_reward.py        */
 #define FGX_REW_VEL_ACC 1    /* hr_dist_vel_acc_reward.py  */
 #define FGX_REW_UNBOUNDED 2  /* hr_unbounded_reward.py     */
+
+/* trajectory validity (ABI 6): the env-side hooks BlackBoxWrapper.step calls before it runs a plan,
+ * RawInterfaceWrapper.preprocessing_and_validity_callback / invalid_traj_callback
+ * (raw_interface_wrapper.py:55-72,103-121; called at black_box_wrapper.py:178-197).  The reachers
+ * keep the identity default (every plan valid, valid_flags = 0); a registered variant can ask for
+ * the checks the reference's overriding envs make (table_tennis_env.py:304-309): */
+#define FGX_VALID_TAU 1    /* valid_tau_lo <= action[0] <= valid_tau_hi (the raw f32 action, compared in
+                              f32 as numpy does a float32 scalar against a Python float); learn_tau  */
+#define FGX_VALID_DELAY 2  /* the same for the delay entry action[learn_tau]; learn_delay              */
+#define FGX_VALID_POS 4    /* valid_pos_lo[d] <= desired position d <= valid_pos_hi[d] at every sample
+                              of the plan (f32 positions against f64 bounds, as numpy compares them) */
+/* the artificial transition of an invalid plan (invalid_traj_callback): no env step is taken,
+ * trajectory_length = 0, return = invalid_reward, flags = invalid_terminated / invalid_truncated,
+ * observation = zeros (the reference default, np.zeros) or the env's current observation */
+#define FGX_INVALID_OBS_ZEROS 0
+#define FGX_INVALID_OBS_CURRENT 1
 
 /* trajectory generators (reference: trajectory_generator_factory.py:7-21) */
 #define FGX_MP_NONE 0   /* step-based env only (fgx_step_raw)                */
@@ -118,7 +134,7 @@ typedef struct fgx_config {
   double pc_length;             /* ProDMP pre_compute_length_factor                         */
   double p_gain, d_gain;        /* PD gains                                                 */
   double act_low, act_high;     /* env action-space bounds as stored by gymnasium Box (f32) */
-  double hole_width, hole_depth, hole_x; /* NaN = sampled at reset (hole_reacher.py:261-294) */
+  double hole_width, hole_depth, hole_x; /* NaN = sampled at reset (hole_reacher.py:79-112)  */
   double collision_penalty;     /* HoleReacher / ViaPointReacher reward                     */
   /* ---- ABI 2 */
   int32_t rew_fct;              /* FGX_REW_* (HoleReacher only)                             */
@@ -142,6 +158,13 @@ typedef struct fgx_config {
   int32_t n_gains;
   int32_t reserved1;
   double p_gains[8], d_gains[8];
+  /* ---- ABI 6: trajectory validity (FGX_VALID_*, FGX_INVALID_OBS_*) */
+  int32_t valid_flags;          /* 0 = every plan valid (the reachers' RawInterfaceWrapper default) */
+  int32_t invalid_obs;          /* FGX_INVALID_OBS_*                                        */
+  int32_t invalid_terminated, invalid_truncated;
+  double invalid_reward;
+  double valid_tau_lo, valid_tau_hi, valid_delay_lo, valid_delay_hi;
+  double valid_pos_lo[8], valid_pos_hi[8];
 } fgx_config;
 
 typedef struct fgx_dims {
@@ -226,7 +249,9 @@ int fgx_get_tables(void* handle, float* out, void* stream);
  * arrays): 0 = k_episode (one env per lane), 1 = k_episode_jp (one wave per joint),
  * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs), 3 = k_episode_jl (one lane
  * per env x joint), 4 = k_episode_w2 (k_episode for two resident waves per SIMD); negative on error.
- * All three give bit-identical results; the choice follows measured speed (fgx_dispatch.h). */
+ * info_level >= 1 means some per-step output pointer is given (the launch then runs the logging
+ * k_episode, as it does for a config with valid_flags).  All five give bit-identical results; the
+ * choice follows measured speed (fgx_dispatch.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 
 #ifdef __cplusplus

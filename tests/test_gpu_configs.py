@@ -33,6 +33,9 @@ CONFIGS = [
     ("metric_shard2", "fancy_ProMP/LongSimpleReacher-v0", None, 32768, 2, "k_episode_jl"),
     ("metric_shard4", "fancy_ProMP/LongSimpleReacher-v0", None, 16384, 2, "k_episode_jl"),
     ("metric_shard8", "fancy_ProMP/LongSimpleReacher-v0", None, 8192, 2, "k_episode_jl"),
+    # past one round of waves: k_episode_w2 directly against the oracle (config 4 unsharded on one GPU)
+    ("config4_one_gpu", "fancy_DMP/LongSimpleReacher-v0", None, 262144, 2, "k_episode_w2"),
+    ("metric_x2", "fancy_ProMP/LongSimpleReacher-v0", None, 131072, 2, "k_episode_w2"),
 ]
 
 

@@ -252,6 +252,31 @@ def test_fast_path_guard_restored_extreme_state(monkeypatch):
                                               for _ in range(2)], setup=setup)
 
 
+@pytest.mark.parametrize("kernel", ["classic", "jl"])
+def test_fast_path_guard_weights_scale(monkeypatch, kernel):
+    """trajectory_generator_kwargs weights_scale = 1e12 is carried by the ProMP table
+    (table = f32(weights_scale * phi)): a lane with |w| ~ 1e28 overflows its f32 position to inf
+    (velocity NaN, u NaN, np.clip keeps it).  The NaN-free guard bounds |w| by 1e30 / (the table's
+    largest row L1 norm), so that wave takes the exact path; waves of ordinary weights (positions
+    ~1e12, controls clipped to +-1000) stay in the fast blocks.  k_episode and k_episode_jl."""
+    monkeypatch.setenv("FGX_EPISODE_KERNEL", kernel)
+    over = {"trajectory_generator_kwargs": {"weights_scale": 1e12}}
+    N = 256
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, info_level=0,
+                   mp_config_override=over)
+    assert env.episode_kernel() == {"classic": "k_episode", "jl": "k_episode_jl"}[kernel]
+    assert float(np_(env.tables())[:, :5].max()) > 1e10
+    rng = np.random.default_rng(12)
+    plist = []
+    for b in range(2):
+        p = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        p[64 + 9, 3] = np.float32(1e28)
+        p[130, 20] = np.float32(-3e27)
+        p[192:256] *= np.float32(1e-9)
+        plist.append(p)
+    _run_vs_oracle(env, "LongSimpleReacher", plist)
+
+
 # ------------------------------------------------------------------------------ reset_mask / checks
 def test_reset_mask_rows_and_length_checks():
     N = 96

@@ -1,0 +1,170 @@
+"""Trajectory validity (RawInterfaceWrapper.preprocessing_and_validity_callback /
+invalid_traj_callback, raw_interface_wrapper.py:55-72,103-121, called at black_box_wrapper.py:178-197)
+on the device, the ProDMP delay guard, and the device reward aggregations at full size.
+
+* The device's choice of invalid plans equals the host predicate fgx.TrajValidity.__call__ (the
+  numpy form of table_tennis_env.py:304-309) applied to each env's action and plan
+  (env.trajectory, the same plan the step runs).
+* An invalid plan is the artificial transition: trajectory_length 0, the configured return and
+  flags, zeros / the current observation, no env step (state unchanged) and, when the flags end
+  the episode, the VectorEnv auto-reset (final observation = the artificial one).
+* Valid envs of the same batch are bit-identical to a run without the validity checks.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fancy_gym_crowd_amd as fgx
+from tests.test_gpu_parity import DEV, np_
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(env_id, N, validity, over=None, seed=7, **kw):
+    a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, traj_validity=validity, **kw)
+    b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, **kw)
+    a.reset(seed=seed)
+    b.reset(seed=seed)
+    return a, b
+
+
+def _state(env):
+    return {k: np_(v).copy() for k, v in env.get_state().items()}
+
+
+@pytest.mark.parametrize("obs_kind", ["zeros", "current"])
+@pytest.mark.parametrize("info_level", [0, 2])
+def test_position_bounds_artificial_transition(obs_kind, info_level):
+    N = 256
+    lo, hi = [-1.5] * 5, [1.5] * 5
+    val = fgx.TrajValidity(pos_low=lo, pos_high=hi, invalid_return=-7.5, terminated=False, truncated=False,
+                           obs=obs_kind)
+    env, ref = _pair("fancy_ProMP/LongSimpleReacher-v0", N, val, info_level=info_level)
+    assert env.episode_kernel() == "k_episode"   # validity runs in the logging k_episode
+    rng = np.random.default_rng(5)
+    for b in range(3):
+        p = rng.standard_normal((N, env.n_params), dtype=np.float32) * np.float32(0.6)
+        p[::3] *= np.float32(4.0)   # a third of the envs with large weights
+        pt = torch.from_numpy(p).to(DEV)
+        pos, vel = env.trajectory(pt)
+        want_valid = np.array([val(p[i], np_(pos[i]), np_(vel[i]))[0] for i in range(N)])
+        assert 0 < want_valid.sum() < N
+        obs_before = np_(env.reset(options={"reset_mask": np.zeros(N, bool)})[0])
+        st0 = _state(env)
+        obs, ret, te, tr, info = env.step(pt)
+        tl = np_(info["trajectory_length"])
+        np.testing.assert_array_equal(tl > 0, want_valid)
+        inv = ~want_valid
+        np.testing.assert_array_equal(np_(ret)[inv], -7.5)
+        assert not np_(te)[inv].any() and not np_(tr)[inv].any()
+        exp_obs = obs_before[inv] if obs_kind == "current" else np.zeros_like(obs_before[inv])
+        np.testing.assert_array_equal(np_(obs)[inv], exp_obs)
+        np.testing.assert_array_equal(np_(info["final_observation"])[inv], exp_obs)
+        st1 = _state(env)
+        for k in ("q", "qd", "goal", "steps"):   # no env step for an invalid plan
+            np.testing.assert_array_equal(st1[k][inv], st0[k][inv])
+        if info_level >= 2:
+            assert np.isnan(np_(info["step_rewards"])[inv]).all()
+        if b == 0:   # valid envs: bit-identical to the same fresh envs without validity checks
+            r_obs, r_ret, r_te, r_tr, r_info = ref.step(pt)
+            ok = want_valid
+            np.testing.assert_array_equal(np_(ret)[ok], np_(r_ret)[ok])
+            np.testing.assert_array_equal(np_(obs)[ok], np_(r_obs)[ok])
+            np.testing.assert_array_equal(np_(info["final_observation"])[ok], np_(r_info["final_observation"])[ok])
+            np.testing.assert_array_equal(tl[ok], np_(r_info["trajectory_length"])[ok])
+            for k in ("q", "qd", "goal", "steps"):
+                np.testing.assert_array_equal(st1[k][ok], _state(ref)[k][ok])
+
+
+def test_tau_delay_bounds_and_autoreset():
+    """Raw learned tau / delay entries (before the action-space clip) against validity bounds; the
+    default artificial flags (terminated=True) end the episode, so the VectorEnv auto-resets the env:
+    final observation = zeros, the new observation = a fresh reset."""
+    over = {"phase_generator_kwargs": {"learn_tau": True, "learn_delay": True}}
+    N = 192
+    val = fgx.TrajValidity(tau=(0.5, 1.5), delay=(0.0, 0.4))
+    env, ref = _pair("fancy_ProDMP/SimpleReacher-v0", N, val, over=over, info_level=0)
+    assert env.n_params == 2 + 2 * 6
+    rng = np.random.default_rng(11)
+    p = rng.standard_normal((N, env.n_params), dtype=np.float32)
+    p[:, 0] = rng.uniform(0.2, 1.8, N).astype(np.float32)
+    p[:, 1] = rng.uniform(-0.2, 0.6, N).astype(np.float32)
+    p[:3, :2] = np.array([[1.5, 0.1], [0.5, 0.1], [1.0, 0.4]], np.float32)   # on the bounds: valid
+    pt = torch.from_numpy(p).to(DEV)
+    pos, vel = env.trajectory(pt)
+    want_valid = np.array([val(p[i], np_(pos[i]), np_(vel[i]), learn_tau=True)[0] for i in range(N)])
+    assert want_valid[:3].all() and 0 < want_valid.sum() < N
+    obs, ret, te, tr, info = env.step(pt)
+    tl = np_(info["trajectory_length"])
+    inv = ~want_valid
+    np.testing.assert_array_equal(tl > 0, want_valid)
+    np.testing.assert_array_equal(np_(ret)[inv], 0.0)
+    assert np_(te)[inv].all() and not np_(tr)[inv].any()
+    np.testing.assert_array_equal(np_(info["final_observation"])[inv], 0.0)
+    assert np_(info["_final_observation"])[inv].all()
+    st = _state(env)
+    assert (st["steps"][inv] == 0).all()
+    # the auto-reset observation of an invalid env is the reset continuation of its own stream: the
+    # same as the reference env's after an explicit unseeded reset of those envs
+    o_ref, _ = ref.reset(options={"reset_mask": inv})
+    np.testing.assert_array_equal(np_(obs)[inv], np_(o_ref)[inv])
+
+
+def test_validity_config_errors():
+    with pytest.raises(ValueError):   # tau check without a learned tau
+        fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=4, device=DEV, traj_validity=fgx.TrajValidity(tau=(0, 1)))
+    with pytest.raises(ValueError):
+        fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=4, device=DEV,
+                 traj_validity=fgx.TrajValidity(pos_low=[0, 0, 0], pos_high=[1, 1, 1]))
+
+
+@pytest.mark.parametrize("delay", [-0.1, float("nan"), float("inf")])
+def test_prodmp_negative_or_nonfinite_delay_refused(delay):
+    """A static delay < 0 would look up basis rows past the current one (prodmp_delay_index);
+    fgx_create refuses it (FGX_E_INVALID -> ValueError)."""
+    with pytest.raises(ValueError, match="delay"):
+        fgx.make("fancy_ProDMP/SimpleReacher-v0", num_envs=8, device=DEV,
+                 mp_config_override={"phase_generator_kwargs": {"delay": delay}})
+
+
+# ------------------------------------------------------------------------------ device aggregation
+@pytest.mark.parametrize("agg", [np.max, np.min, np.median])
+def test_device_reward_aggregation_matches_numpy(agg):
+    """np.max / np.min / np.median of rewards[:t+1] (black_box_wrapper.py:252) computed on the device
+    equal numpy applied to the device's own per-step rewards, bit for bit, HoleReacher (ragged
+    lengths from collisions, -100 penalties) and replanning SimpleReacher (segments of 25)."""
+    for env_id, over in (("fancy_ProDMP/HoleReacher-v0", {}),
+                         ("fancy_ProMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}})):
+        over = dict(over)
+        over.setdefault("black_box_kwargs", {})
+        over["black_box_kwargs"] = dict(over["black_box_kwargs"], reward_aggregation=agg)
+        N = 1024
+        env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
+        env.reset(seed=1)
+        rng = np.random.default_rng(2)
+        for b in range(2):
+            p = torch.from_numpy(rng.standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)
+            _, ret, _, _, info = env.step(p)
+            rew = np_(info["step_rewards"])
+            tl = np_(info["trajectory_length"])
+            want = np.array([agg(rew[i, :tl[i]]) for i in range(N)])
+            np.testing.assert_array_equal(np_(ret), want)
+
+
+def test_device_median_at_metric_size_host_time():
+    """np.median at 65536 envs: no per-env host loop (the step's host time stays in milliseconds)."""
+    import time
+    N = 65536
+    over = {"black_box_kwargs": {"reward_aggregation": np.median}}
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    env.reset(seed=0)
+    p = torch.randn((N, env.n_params), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    env.step(p)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, ret, _, _, info = env.step(p)
+    host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    assert "step_rewards" not in info
+    assert host < 0.05, host
+    assert bool(torch.isfinite(ret).all())

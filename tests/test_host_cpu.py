@@ -56,9 +56,32 @@ def test_library_loads_and_reports_abi():
 
 def test_config_struct_layout_matches_header():
     # 20 int32, 18 doubles, (ABI 2) 4 int32 and 8 doubles, (ABI 3) 17 int32 + pad and 8 doubles,
-    # (ABI 4) 2 int32 and 16 doubles
-    assert ctypes.sizeof(_lib.FgxConfig) == 20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8 + 2 * 4 + 16 * 8
+    # (ABI 4) 2 int32 and 16 doubles, (ABI 6) 4 int32 and 21 doubles
+    assert ctypes.sizeof(_lib.FgxConfig) == (20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8 + 2 * 4 + 16 * 8
+                                             + 4 * 4 + 21 * 8)
     assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
+
+
+def test_ctypes_layout_equals_c_compiler_layout(tmp_path):
+    """Every field offset of the ctypes mirrors equals offsetof() of include/fgx.h under gcc."""
+    import subprocess
+    src = tmp_path / "layout.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fgx.h"', 'int main(void) {']
+    for cname, cls in (("fgx_config", _lib.FgxConfig), ("fgx_dims", _lib.FgxDims), ("fgx_info", _lib.FgxInfo)):
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines += ['return 0;', '}']
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                            check=True).stdout.splitlines())
+    for cname, cls in (("fgx_config", _lib.FgxConfig), ("fgx_dims", _lib.FgxDims), ("fgx_info", _lib.FgxInfo)):
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
 
 
 def test_registry_ids():
