@@ -97,6 +97,10 @@ def episode_bytes_per_env(env):
     return reads + writes
 
 
+def env_id_of(env):
+    return env.meta["env_id"]
+
+
 def basis_gemm(env, params, reps=10):
     """The MP basis x weights contraction as its own launch (BlackBoxWrapper.get_trajectory ->
     fgx_trajectory -> k_traj_mfma, v_mfma_f32_32x32x2_f32 with K = 8): time per launch from HIP
@@ -125,7 +129,19 @@ def basis_gemm(env, params, reps=10):
     t = e0.elapsed_time(e1) / reps * 1e-3
     flops = 2 * 2 * 8 * N * n * T                 # two K = 8 GEMMs (positions, next positions)
     out_bytes = 2 * 4 * N * T * n + 4 * N * env.n_params
-    return {"kernel": "k_traj_mfma", "us": t * 1e6, "mfma_tflops": flops / t / 1e12,
+    pmc, note = pmc_entry(env_id_of(env), N, "k_traj_mfma", lib_build_id())
+    counters = None
+    if pmc is not None and pmc.get("mfma_f32_flops"):
+        ns = (pmc.get("kernel_ns_median_under_pmc") or {}).get("mfma")
+        counters = {"mfma_f32_instr": pmc.get("mfma_f32_instr"), "mfma_f32_flops": pmc["mfma_f32_flops"],
+                    "mfma_busy_cycles": pmc.get("mfma_busy_cycles"),
+                    "pmc_flops_over_algorithmic": pmc["mfma_f32_flops"] / flops,
+                    "traffic_bytes_per_launch": pmc.get("traffic_bytes_per_launch"),
+                    "kernel_ns_under_pmc": ns, "source": pmc.get("source")}
+        if ns:
+            counters["pmc_mfma_frac"] = pmc["mfma_f32_flops"] / (ns * 1e-9) / 1e12 / FP32_VEC_PEAK_TF
+    return {"kernel": "k_traj_mfma", "us": t * 1e6, "mfma_tflops": flops / t / 1e12, "pmc": counters,
+            "pmc_note": note,
             "peak_tflops": FP32_VEC_PEAK_TF, "mfma_frac": flops / t / 1e12 / FP32_VEC_PEAK_TF,
             "hbm_GBps": out_bytes / t / 1e9, "hbm_frac": out_bytes / t / 1e9 / HBM_PEAK_GBS,
             "note": "K = 8 (5 basis + zero pad): arithmetic intensity 2 flop/B, bound by the output "

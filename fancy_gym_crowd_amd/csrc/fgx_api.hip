@@ -491,7 +491,7 @@ static Outputs make_outputs(float* obs, double* ret, uint8_t* te, uint8_t* tr, i
   }
 #ifdef FGX_STAMPS
   static unsigned long long* stamps = nullptr;   // diagnostics build only (tools/stamps.py)
-  if (!stamps && hipMalloc(&stamps, 16384 * 8 * sizeof(unsigned long long)) != hipSuccess) stamps = nullptr;
+  if (!stamps && hipMalloc(&stamps, 16384 * 16 * sizeof(unsigned long long)) != hipSuccess) stamps = nullptr;
   o.stamps = stamps;
   g_stamps = stamps;
 #endif

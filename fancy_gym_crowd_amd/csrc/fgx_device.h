@@ -129,14 +129,15 @@ struct Outputs {
 };
 
 // Section clocks of one wave (diagnostics build, -DFGX_STAMPS): lane 0 of wave w stores the shader
-// clock (s_memtime) at point i to stamps[w * 8 + i] with an ordinary vector store.
+// clock (s_memtime) at point i to stamps[w * 16 + i] with an ordinary vector store; points 6 and 7
+// store s_memrealtime (kernel entry / exit), points 8..15 are further shader-clock sections.
 #ifdef FGX_STAMPS
 #define FGX_STAMP(o, e, i)                                                                \
   do {                                                                                    \
-    const unsigned long long t_ = (i) >= 6 ? __builtin_amdgcn_s_memrealtime()             \
-                                           : __builtin_readcyclecounter();                \
+    const unsigned long long t_ = ((i) == 6 || (i) == 7) ? __builtin_amdgcn_s_memrealtime() \
+                                                         : __builtin_readcyclecounter();  \
     if ((threadIdx.x & 63) == 0 && (o).stamps && ((e) >> 6) < 16384)                      \
-      (o).stamps[((e) >> 6) * 8 + (i)] = t_;                                              \
+      (o).stamps[((e) >> 6) * 16 + (i)] = t_;                                             \
   } while (0)
 #else
 #define FGX_STAMP(o, e, i) do { } while (0)

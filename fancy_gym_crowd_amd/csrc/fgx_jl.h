@@ -105,6 +105,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   sg.init(c, s, e, valid);
   const int Lmin = wave_min(valid ? sg.L : 0x7fffffff), Lmax = wave_max(valid ? sg.L : 0);
   const int lead = vmask ? __builtin_ctzll(vmask) : 0;
+  FGX_STAMP(o, wst, 12);
 
   // ---- this lane's joint
   double pg = c.pg[0], dg = c.dg[0];
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
       tg.init(c, pe + d * nb, s.tables, s0, &ic_q, &ic_qd, c.T, c.tau32, c.rcp_tau32, NL * nb + d - d * nb);
   };
   init_traj();
+  FGX_STAMP(o, wst, 13);
   // basis rows through scalar loads when every valid lane's plan starts on the same row
   const int s0u = __builtin_amdgcn_readlane(s0, lead);
   const bool s0_uni = __ballot(valid && s0 != s0u) == 0;
@@ -510,6 +512,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (lane == 0 && sum != 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
   }
   FGX_STAMP(o, wst, 4);
+  FGX_STAMP(o, wst, 8);
   constexpr int R0 = (EPB + 63) / 64 * 64;
   constexpr bool SPLIT = R0 + EPB <= 64 * S::WAVES;
   const bool split = SPLIT && o.autoreset;
@@ -534,12 +537,14 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   if (split) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state reads above have landed
     __syncthreads();
+    FGX_STAMP(o, wst, 9);
     if (rs_do) {   // concurrent with the first group's returns and final observations
       autoreset_env(c, s, er, vr);
       emit_obs(c, vr, c.return_context, o.obs + er * c.out_dim, nullptr, true);
       store_env(c, s, er, vr, false);
       s.plans[er] = 0;
     }
+    FGX_STAMP(o, wst, 10);
   }
   if (!tv) {
     FGX_STAMP(o, wst, 5);
@@ -559,6 +564,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     os_[k] = ga[(25 + 5 * NL + k) * EPB + t];
   }
   v.fk_given(fc, fs);
+  FGX_STAMP(o, wst, 11);
   // the last sample at env step 199 (simple_reacher.py:60-62): r = -dist(ee, goal) - sum a^2; it is
   // the last element of the return sum, either the sequential tail's last or slot 7 of the last
   // 8-block (L == bend)

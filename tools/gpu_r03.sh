@@ -12,6 +12,7 @@ for st in $STAGES; do
     tests) timeout -k 10 ${TEST_TIMEOUT:-1100} python -u -m pytest tests -v -m gpu --maxfail=10 --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$? ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$? ;;
+    stamps) STAMP_RUNS="${STAMP_RUNS:-jl:8192 jl:16384 classic:65536}" bash tools/gpu_stamps.sh > gpurun_out/stamps_run.log 2>&1; rc=$? ;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1; rc=$? ;;
     *) echo "unknown stage $st"; rc=2 ;;
   esac

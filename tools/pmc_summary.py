@@ -1,18 +1,23 @@
 """Build profiles/pmc_summary.json (read by bench.py's roofline) from rocprofv3 --pmc passes.
 
-  python tools/pmc_summary.py gpurun_out/pmc_r02 [--round r02]
+  python tools/pmc_summary.py gpurun_out/pmc_r03 [--round r03]
 
-Expects, per profiled size, the sub-directories written by tools/gpu_pmc_r02.sh:
-  <src>/n<ENVS>/fetch/*_counter_collection.csv    (--pmc FETCH_SIZE)
-  <src>/n<ENVS>/write/*_counter_collection.csv    (--pmc WRITE_SIZE)
-  <src>/n<ENVS>/issue/*_counter_collection.csv    (--pmc SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE)
-  <src>/n<ENVS>/busy/*_counter_collection.csv     (--pmc VALUBusy)
-each a separate rocprofv3 pass over `bench.py --global-envs ENVS --no-cpu-baseline`.
+Expects, per profiled case, a directory <src>/<case>/ holding `workload.txt` (the env id; default
+the metric's) and the sub-directories written by tools/gpu_pmc_r03.sh, one rocprofv3 pass each over
+`bench.py --env-id ID --global-envs ENVS --no-cpu-baseline`:
+  fetch/  --pmc FETCH_SIZE
+  write/  --pmc WRITE_SIZE
+  issue/  --pmc SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE
+  busy/   --pmc VALUBusy
+  mix/    --pmc SQ_INSTS_VALU SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64
+  mfma/   --pmc SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES   (k_traj_mfma)
+Case directory names are n<ENVS> or n<ENVS>_<tag>.
 
 Per counter the value of one dispatch is the sum over its rows (instances / XCDs); the entry keeps
-the median over the episode-kernel dispatches of the pass.  HBM traffic follows
-MI355X_MICROARCH.md's HBM/rocprofv3 recipe: FETCH_SIZE and WRITE_SIZE in KiB, FETCH_SIZE doubled
-(gfx950 counts half the fetched 64-B lines), bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+the median over the dispatches of the profiled kernel.  HBM traffic follows MI355X_MICROARCH.md's
+HBM/rocprofv3 recipe: FETCH_SIZE and WRITE_SIZE in KiB, FETCH_SIZE doubled (gfx950 counts half the
+fetched 64-B lines), bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The VALU mix: f64 = ADD + MUL +
+FMA + TRANS f64 instructions, cvt = conversions (bench.py prices both at the f64 issue rate).
 """
 import argparse
 import collections
@@ -26,22 +31,25 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "fancy_ProMP/LongSimpleReacher-v0"
 T = 200
+PARTS = ("fetch", "write", "issue", "busy", "mix", "mfma")
 
 
 def kernel_family(name):
     """'fgx::k_episode_jp<1, 5, 5>(...)' -> 'k_episode_jp' (the name env.episode_kernel() reports)."""
-    m = re.search(r"(k_episode(?:_jp|_ws|_jl)?)\b", name)
+    m = re.search(r"(k_episode(?:_jp|_ws|_jl|_w2)?|k_traj_mfma)\b", name)
     return m.group(1) if m else None
 
 
-def per_dispatch(src):
-    """{counter: median per-dispatch value}, median kernel ns, kernel family, full kernel name."""
+def per_dispatch(src, want=None):
+    """{counter: median per-dispatch value}, median kernel ns, kernel family, full kernel name.
+    want: the kernel family to keep (default: the first episode / trajectory kernel seen)."""
     vals, durs, fam, full = collections.defaultdict(list), [], None, None
     for path in sorted(glob.glob(os.path.join(src, "**", "*_counter_collection.csv"), recursive=True)):
         agg, dur = collections.defaultdict(float), {}
         for r in csv.DictReader(open(path)):
             f = kernel_family(r["Kernel_Name"])
-            if f is None:
+            if f is None or (want is not None and f != want) or (want is None and f == "k_traj_mfma") or \
+                    (fam is not None and f != fam):
                 continue
             fam, full = f, r["Kernel_Name"]
             agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
@@ -63,50 +71,78 @@ def build_id():
         return None
 
 
+def entry(d, envs, workload, bid, rnd, want=None):
+    counters, ns, fam, full = {}, {}, None, None
+    for part in PARTS:
+        if not os.path.isdir(os.path.join(d, part)):
+            continue
+        med, kns, f, k = per_dispatch(os.path.join(d, part), want)
+        counters.update(med)
+        ns[part] = kns
+        fam, full = fam or f, full or k
+    if fam is None:
+        return None
+    e = {"workload": workload, "envs": envs, "kernel": fam, "kernel_name": full,
+         "build_id": bid, "kernel_ns_median_under_pmc": ns,
+         "counters_per_dispatch": counters,
+         "source": f"profiles/{rnd}_pmc/{os.path.basename(d)}"}
+    if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+        e["FETCH_SIZE_KiB"] = counters["FETCH_SIZE"]
+        e["WRITE_SIZE_KiB"] = counters["WRITE_SIZE"]
+        e["traffic_bytes_per_launch"] = (2 * counters["FETCH_SIZE"] + counters["WRITE_SIZE"]) * 1024.0
+    if "SQ_INSTS_VALU" in counters:
+        e["valu_instr_per_launch"] = counters["SQ_INSTS_VALU"]
+        e["waves"] = counters.get("SQ_WAVES")
+        e["valu_instr_per_inner_step_per_env"] = counters["SQ_INSTS_VALU"] * 64 / envs / T
+    if "SQ_INSTS_VALU_CVT" in counters:
+        f64 = sum(counters.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
+        e["valu_mix"] = {"f64": f64, "cvt": counters["SQ_INSTS_VALU_CVT"],
+                         "int64": counters.get("SQ_INSTS_VALU_INT64"),
+                         "total_same_pass": counters.get("SQ_INSTS_VALU")}
+        e["valu_mix_source"] = "PMC SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 + SQ_INSTS_VALU_CVT"
+    if "VALUBusy" in counters:
+        e["valu_busy_pct"] = counters["VALUBusy"]
+    if "SQ_INSTS_VALU_MFMA_MOPS_F32" in counters:
+        e["mfma_f32_instr"] = counters.get("SQ_INSTS_VALU_MFMA_F32")
+        e["mfma_f32_flops"] = counters["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
+        e["mfma_busy_cycles"] = counters.get("SQ_VALU_MFMA_BUSY_CYCLES")
+    return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r03")
     ap.add_argument("--build-id", default=None, help="build id of the profiled library (default: the "
                     "hash of the sources in this tree)")
     a = ap.parse_args()
     bid = a.build_id or build_id()
     entries = []
     for d in sorted(glob.glob(os.path.join(a.src, "n*"))):
-        envs = int(os.path.basename(d)[1:])
-        counters, ns, fam, full = {}, {}, None, None
-        for part in ("fetch", "write", "issue", "busy"):
-            med, kns, f, k = per_dispatch(os.path.join(d, part))
-            counters.update(med)
-            ns[part] = kns
-            fam, full = fam or f, full or k
-        if fam is None:
-            continue
-        e = {"workload": WORKLOAD, "envs": envs, "kernel": fam, "kernel_name": full,
-             "build_id": bid, "kernel_ns_median_under_pmc": ns,
-             "counters_per_dispatch": counters,
-             "source": f"profiles/{a.round}_pmc/n{envs}"}
-        if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
-            e["FETCH_SIZE_KiB"] = counters["FETCH_SIZE"]
-            e["WRITE_SIZE_KiB"] = counters["WRITE_SIZE"]
-            e["traffic_bytes_per_launch"] = (2 * counters["FETCH_SIZE"] + counters["WRITE_SIZE"]) * 1024.0
-        if "SQ_INSTS_VALU" in counters:
-            e["valu_instr_per_launch"] = counters["SQ_INSTS_VALU"]
-            e["waves"] = counters.get("SQ_WAVES")
-            e["valu_instr_per_inner_step_per_env"] = counters["SQ_INSTS_VALU"] * 64 / envs / T
-        if "VALUBusy" in counters:
-            e["valu_busy_pct"] = counters["VALUBusy"]
-        entries.append(e)
-    out = {"method": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc_r02.sh); median over "
+        envs = int(re.match(r"n(\d+)", os.path.basename(d)).group(1))
+        wl = os.path.join(d, "workload.txt")
+        workload = open(wl).read().strip() if os.path.exists(wl) else WORKLOAD
+        if os.path.isdir(os.path.join(d, "mfma")):   # the basis GEMM launch of the same bench run
+            e = entry(d, envs, workload, bid, a.round, want="k_traj_mfma")
+            if e is not None:
+                entries.append(e)
+        e = entry(d, envs, workload, bid, a.round)
+        if e is not None and e["kernel"] != "k_traj_mfma":
+            entries.append(e)
+    out = {"method": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc_r03.sh); median over "
                      "dispatches of the per-dispatch sum over instances; traffic = (2*FETCH_SIZE + "
-                     "WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count)", "entries": entries}
+                     "WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count); valu_mix from the mix pass",
+           "entries": entries}
     # the counter CSVs the entries come from travel with the summary
     for d in sorted(glob.glob(os.path.join(a.src, "n*"))):
+        dd0 = os.path.join(ROOT, "profiles", f"{a.round}_pmc", os.path.basename(d))
         for path in glob.glob(os.path.join(d, "*", "**", "*_counter_collection.csv"), recursive=True):
             part = os.path.relpath(path, d).split(os.sep)[0]
-            dd = os.path.join(ROOT, "profiles", f"{a.round}_pmc", os.path.basename(d), part)
-            os.makedirs(dd, exist_ok=True)
-            shutil.copy(path, os.path.join(dd, os.path.basename(path)))
+            os.makedirs(os.path.join(dd0, part), exist_ok=True)
+            shutil.copy(path, os.path.join(dd0, part, os.path.basename(path)))
+        if os.path.exists(os.path.join(d, "workload.txt")):
+            os.makedirs(dd0, exist_ok=True)
+            shutil.copy(os.path.join(d, "workload.txt"), os.path.join(dd0, "workload.txt"))
     dst = os.path.join(ROOT, "profiles", "pmc_summary.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)

@@ -52,10 +52,12 @@ if kern == "k_episode_jl":
     W = (N + epb - 1) // epb * 4
 else:
     W = (N + 63) // 64
-buf = np.zeros(W * 8, dtype=np.uint64)
-assert fn(buf.ctypes.data, W * 8) == 0
-st = buf.reshape(W, 8)[:, :6].astype(np.int64)
-rt = buf.reshape(W, 8)[:, 6:].astype(np.int64)   # s_memrealtime (100 MHz, one clock for the GPU)
+buf = np.zeros(W * 16, dtype=np.uint64)
+assert fn(buf.ctypes.data, W * 16) == 0
+full = buf.reshape(W, 16).astype(np.int64)
+st = full[:, :6]
+rt = full[:, 6:8]   # s_memrealtime (100 MHz, one clock for the GPU)
+extra = full[:, 8:]  # further shader-clock points (0 = not stamped by this kernel)
 names = (["prologue", "fast_chunks", "slow_chunks", "gather", "return_epilogue"] if kern == "k_episode_jl" else
          ["prologue", "fast_blocks", "generic_samples", "return", "epilogue"])
 sec = np.diff(st, axis=1)
@@ -91,4 +93,15 @@ out["realtime_us"] = {"start_max": float(rstart.max() / 100), "start_median": fl
                       "wave_duration_median": float(np.median(rend - rstart) / 100)}
 out["shader_ticks_per_us"] = float(np.median((st[:, 5] - st[:, 0]) / np.maximum(1, rt[:, 1] - rt[:, 0]) * 100))
 out["ticks_per_us_upper_bound"] = max(p["span"] for p in per) / kern_us
+# extra points 8..15: median cycles since kernel entry, per wave slot of the workgroup (jl: 4 waves)
+ws = 4 if kern == "k_episode_jl" else 1
+pts = {}
+for i in range(8):
+    col = extra[:, i]
+    if (col != 0).any():
+        pts[str(8 + i)] = {f"wave{w}": int(np.median((col - st[:, 0])[w::ws][col[w::ws] != 0]))
+                           for w in range(ws) if (col[w::ws] != 0).any()}
+if pts:
+    out["points_since_entry"] = pts
+    out["point5_since_entry"] = {f"wave{w}": int(np.median((st[:, 5] - st[:, 0])[w::ws])) for w in range(ws)}
 print(json.dumps(out), flush=True)
