@@ -18,7 +18,7 @@ from .registry import (ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS, ENV_SPECS, KNOWN_MPS
                        upgrade)
 
 __all__ = ["make", "BlackBoxVectorEnv", "StepVectorEnv", "ReplanEvery", "ReplanAt", "ReplanNormPeriod",
-           "ReplanAny", "REPLAN_CLOSE", "TrajValidity", "register", "upgrade", "resolve",
+           "ReplanAny", "REPLAN_CLOSE", "TrajValidity", "register", "register_gymnasium", "SingleEnv", "upgrade", "resolve",
            "ALL_MOVEMENT_PRIMITIVE_ENVIRONMENTS", "KNOWN_MPS"]
 
 
@@ -34,7 +34,16 @@ def make(env_id, num_envs=1, device="cuda", mp_config_override=None, **kwargs):
     return BlackBoxVectorEnv(env_id, num_envs, device=device, mp_config_override=mp_config_override, **kwargs)
 
 
+def register_gymnasium(device="cuda:0", gym_module=None):
+    """gym.make('fancy_ProMP/...') reachability (envs/registry.py:245-254): see gym_compat."""
+    from .gym_compat import register_gymnasium as _reg
+    return _reg(device, gym_module)
+
+
 def __getattr__(name):
+    if name == "SingleEnv":
+        from .gym_compat import SingleEnv
+        return SingleEnv
     if name in ("BlackBoxVectorEnv", "StepVectorEnv", "Box", "ResetNeeded"):
         from . import vector_env
         return getattr(vector_env, name)

@@ -81,7 +81,8 @@ EXPORTS = {
     "fgx_get_tables": (ctypes.c_int, [ctypes.c_void_p] * 3),
     "fgx_episode_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
 }
-EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2"}
+EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2",
+                   5: "k_episode_jl_pc"}
 
 _LIB = None
 

@@ -505,12 +505,14 @@ struct Env {
     return hit;
   }
 
-  // hole_reacher.py:308-361.  Points of link k: p_j = (c_k*lin_j + jx_k, s_k*lin_j + jy_k),
-  // j = 0..99, with p_0 = joint k and p_99 = joint k+1 exactly.  Both coordinates are monotone
-  // in j (lin_j increases and rounding is monotone), so every atomic test (px < left, py < 0, ...)
-  // holds on a prefix or a suffix of 0..99: each is found by a 7-step binary search over the very
-  // same point expressions, and the three wall conditions become interval intersections.  A
-  // link whose two end joints have y >= 0 cannot reach below the ground and is skipped.
+  // hole_reacher.py:126-179 (_get_line_points, check_wall_collision).  Points of link k:
+  // p_j = (c_k*lin_j + jx_k, s_k*lin_j + jy_k), j = 0..99, with p_0 = joint k and p_99 = joint k+1
+  // exactly.  Both coordinates are monotone in j (lin_j increases and rounding is monotone), so every
+  // atomic test (px < left, py < 0, ...) holds on a prefix or a suffix of 0..99: its boundary is the
+  // real-valued crossing, confirmed by evaluating the very same point expressions on both sides of it
+  // (a 7-step binary search where that check fails), and the three wall conditions become interval
+  // intersections.  A link whose two end joints have y >= 0 cannot reach below the ground and is
+  // skipped.
   __device__ __forceinline__ bool wall_collision(const DevCfg& cf) const {
     const double left = hx - hw / 2, right = hx + hw / 2, nd = -hd;
     bool hit = false;
@@ -524,8 +526,14 @@ struct Env {
       auto lin = [](int j) { return j == 99 ? 1.0 : (double)j * (1.0 / 99.0); };
       auto px = [&](int j) { return ck * lin(j) + bx; };
       auto py = [&](int j) { return sk * lin(j) + by; };
-      // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none
-      auto first = [&](auto pred) {
+      // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none: the estimate je
+      // (the real-valued crossing, rounded up) is checked with two evaluations of the very same point
+      // expressions -- pred(je - 1) false and pred(je) true -- and only a lane whose estimate misses
+      // (a crossing within rounding of a point, NaN / inf state) runs the 7-step binary search
+      auto first = [&](auto pred, float est) {
+        const int je = (est > 0.0f) ? ((est < 100.0f) ? (int)__builtin_ceilf(est) : 100) : 0;
+        const bool ok = (je == 0 || !pred(je - 1)) && (je == 100 || pred(je));
+        if (__builtin_expect(ok, 1)) return je;
         int lo = 0, hi = 100;
 #pragma unroll
         for (int it = 0; it < 7; ++it) {
@@ -535,24 +543,28 @@ struct Env {
         }
         return lo;
       };
+      // real-valued index where f(j) = b + k j / 99 crosses t (an estimate only)
+      const float rck = __builtin_amdgcn_rcpf((float)ck) * 99.0f, rsk = __builtin_amdgcn_rcpf((float)sk) * 99.0f;
+      auto cross = [](double t, double b, float r) { return (float)(t - b) * r; };
       // {j : f(j) < t} / {j : f(j) > t} as [lo, hi) for f monotone with slope sign of `dir`
-      auto below = [&](auto f, double dir, double t, int& lo, int& hi) {
-        if (dir > 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) < t); }); }
-        else if (dir < 0.0) { lo = first([&](int j) { return f(j) < t; }); hi = 100; }
+      auto below = [&](auto f, double dir, double t, float est, int& lo, int& hi) {
+        if (dir > 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) < t); }, est); }
+        else if (dir < 0.0) { lo = first([&](int j) { return f(j) < t; }, est); hi = 100; }
         else { lo = 0; hi = (f(0) < t) ? 100 : 0; }   // constant (or NaN) along the link
       };
-      auto above = [&](auto f, double dir, double t, int& lo, int& hi) {
-        if (dir > 0.0) { lo = first([&](int j) { return f(j) > t; }); hi = 100; }
-        else if (dir < 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) > t); }); }
+      auto above = [&](auto f, double dir, double t, float est, int& lo, int& hi) {
+        if (dir > 0.0) { lo = first([&](int j) { return f(j) > t; }, est); hi = 100; }
+        else if (dir < 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) > t); }, est); }
         else { lo = 0; hi = (f(0) > t) ? 100 : 0; }
       };
       int xl0, xl1, xr0, xr1, xL0, xL1, xR0, xR1, yg0, yg1, yd0, yd1;
-      below(px, ck, left, xl0, xl1);    // px < left
-      above(px, ck, right, xr0, xr1);   // px > right
-      above(px, ck, left, xL0, xL1);    // px > left
-      below(px, ck, right, xR0, xR1);   // px < right
-      below(py, sk, 0.0, yg0, yg1);     // py < 0
-      below(py, sk, nd, yd0, yd1);      // py < -depth
+      const float el = cross(left, bx, rck), er = cross(right, bx, rck);
+      below(px, ck, left, el, xl0, xl1);    // px < left
+      above(px, ck, right, er, xr0, xr1);   // px > right
+      above(px, ck, left, el, xL0, xL1);    // px > left
+      below(px, ck, right, er, xR0, xR1);   // px < right
+      below(py, sk, 0.0, cross(0.0, by, rsk), yg0, yg1);   // py < 0
+      below(py, sk, nd, cross(nd, by, rsk), yd0, yd1);     // py < -depth
       const bool c1 = max(xl0, yg0) < min(xl1, yg1);
       const bool c2 = max(xr0, yg0) < min(xr1, yg1);
       const bool c3 = max(max(xL0, xR0), yd0) < min(min(xL1, xR1), yd1);

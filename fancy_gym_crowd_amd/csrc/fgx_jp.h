@@ -64,9 +64,14 @@ struct JpSeg {
   uint32_t flags;
   bool stop;   // the segment ends in truncation or a replanning sample (black_box_wrapper.py:233-239)
   __device__ __forceinline__ void init(const DevCfg& c, const DevState& s, int64_t e, bool valid) {
-    steps = s.steps[e];
-    flags = s.flags[e];
-    plans = s.plans[e] + 1;
+    init_vals(c, s.steps[e], s.flags[e], s.plans[e], valid);
+  }
+  // the same from the env's stored steps / flags / plan count (values gathered elsewhere)
+  __device__ __forceinline__ void init_vals(const DevCfg& c, int steps_, uint32_t flags_, int plans_stored,
+                                            bool valid) {
+    steps = steps_;
+    flags = flags_;
+    plans = plans_stored + 1;
     const bool plans_ok = c.replan && (c.max_plans <= 0 || plans < c.max_plans);
     k_replan = plans_ok ? first_static_replan(c, steps) : -1;
     L = min(c.T, max(1, c.max_steps - steps));

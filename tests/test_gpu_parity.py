@@ -23,6 +23,11 @@ def np_(t):
     return t.detach().cpu().numpy()
 
 
+def kernel_is(got, want):
+    """episode kernel name check; k_episode_jl_pc is k_episode_jl's producer / consumer form"""
+    return got == want or (want == "k_episode_jl" and got == "k_episode_jl_pc")
+
+
 def close(a, b, rtol=RTOL, atol=1e-6):
     np.testing.assert_allclose(np.asarray(a, np.float64), np.asarray(b, np.float64), rtol=rtol, atol=atol)
 

@@ -208,3 +208,19 @@ def test_per_joint_gains_resolution():
     assert c.n_gains == 0 and (c.p_gain, c.d_gain) == (0.6, 0.075)
     with pytest.raises(ValueError):   # (2,) gains do not broadcast against 5 joints
         fgx.resolve("fancy_ProMP/LongSimpleReacher-v0", {"controller_kwargs": {"p_gains": (1.0, 2.0)}})
+
+
+def test_register_gymnasium_with_stand_in():
+    """envs/registry.py:245-254: every id reaches gym.make; without gymnasium nothing is registered."""
+    import types
+    calls = []
+    stand_in = types.SimpleNamespace(Env=object, register=lambda **kw: calls.append(kw))
+    assert fgx.register_gymnasium(gym_module=stand_in) is True
+    ids = [c["id"] for c in calls]
+    assert "fancy_ProMP/LongSimpleReacher-v0" in ids and "fancy/HoleReacher-v0" in ids
+    assert len(ids) == len(set(ids)) == 4 + 12
+    assert all(callable(c["entry_point"]) for c in calls)
+    try:
+        import gymnasium  # noqa: F401
+    except ImportError:
+        assert fgx.register_gymnasium() is False

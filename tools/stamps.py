@@ -47,18 +47,24 @@ fn = lib.fgx_dbg_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 kern = env.episode_kernel()
-if kern == "k_episode_jl":
+JL = kern in ("k_episode_jl", "k_episode_jl_pc")
+wpb = 8 if kern == "k_episode_jl_pc" else 4   # stamped waves per workgroup (joint waves [+ producers])
+if JL:
     epb = 4 * (64 // env._eng.cfg.n_links)
-    W = (N + epb - 1) // epb * 4
+    W = (N + epb - 1) // epb * wpb
 else:
     W = (N + 63) // 64
 buf = np.zeros(W * 16, dtype=np.uint64)
 assert fn(buf.ctypes.data, W * 16) == 0
 full = buf.reshape(W, 16).astype(np.int64)
+if JL and wpb == 8:   # the joint (consumer) waves carry the sections; producers: points only
+    prod = full[(np.arange(W) % 8) >= 4]
+    full = full[(np.arange(W) % 8) < 4]
+    W = full.shape[0]
 st = full[:, :6]
 rt = full[:, 6:8]   # s_memrealtime (100 MHz, one clock for the GPU)
 extra = full[:, 8:]  # further shader-clock points (0 = not stamped by this kernel)
-names = (["prologue", "fast_chunks", "slow_chunks", "gather", "return_epilogue"] if kern == "k_episode_jl" else
+names = (["prologue", "fast_chunks", "slow_chunks", "gather", "return_epilogue"] if JL else
          ["prologue", "fast_blocks", "generic_samples", "return", "epilogue"])
 sec = np.diff(st, axis=1)
 out = {"env": env_id, "envs": N, "kernel": env.episode_kernel(), "waves": W,
@@ -73,7 +79,7 @@ out["slowest10pct_cycles_median"] = {n: int(np.median(sec[slow, i])) for i, n in
 out["fastest10pct_cycles_median"] = {n: int(np.median(sec[fast, i])) for i, n in enumerate(names)}
 out["slowest10pct_xcd_hist"] = np.bincount(((slow // 4) % 8), minlength=8).tolist()
 out["total_cycles_pctl"] = [int(np.percentile(tot, p)) for p in (0, 10, 50, 90, 100)]
-if kern == "k_episode_jl":   # the epilogue runs in wave 0 of each workgroup
+if JL:   # the epilogue runs in wave 0 of each workgroup
     out["cycles_median_wave0"] = {n: int(np.median(sec[::4, i])) for i, n in enumerate(names)}
 # s_memtime counters are per XCD (workgroup b runs on XCD b % 8): start / end spread inside each
 # XCD, and the clock rate implied by the XCD's first start to last end over the event time
@@ -94,7 +100,7 @@ out["realtime_us"] = {"start_max": float(rstart.max() / 100), "start_median": fl
 out["shader_ticks_per_us"] = float(np.median((st[:, 5] - st[:, 0]) / np.maximum(1, rt[:, 1] - rt[:, 0]) * 100))
 out["ticks_per_us_upper_bound"] = max(p["span"] for p in per) / kern_us
 # extra points 8..15: median cycles since kernel entry, per wave slot of the workgroup (jl: 4 waves)
-ws = 4 if kern == "k_episode_jl" else 1
+ws = 4 if JL else 1
 pts = {}
 for i in range(8):
     col = extra[:, i]
