@@ -249,7 +249,7 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     te = torch.empty(N, dtype=torch.uint8, device=dev)
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     tl = torch.empty(N, dtype=torch.int32, device=dev)
-    acc = torch.zeros(1, dtype=torch.int64, device=dev)   # device counter of inner env steps
+    acc = env.new_inner_steps()   # device counter of inner env steps
 
     for _ in range(W):
         env.step_into(params, obs, ret, te, tr, tl, fobs)
@@ -290,7 +290,7 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    inner_local = int(acc.item())
+    inner_local = int(acc.sum().item())
     if graph is not None:
         kern_ms = ev0[0].elapsed_time(ev1[0]) / K
     else:

@@ -11,7 +11,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 6
+FGX_ABI_VERSION = 7
+INNER_STEPS_LEN = 128 * 16   # include/fgx.h FGX_INNER_STEPS_LEN (partial counters, sum them)
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
 SCHED_EVERY, SCHED_AT, SCHED_NORM_PERIOD = 0, 1, 2
@@ -80,9 +81,9 @@ EXPORTS = {
     "fgx_set_state": (ctypes.c_int, [ctypes.c_void_p] * 7),
     "fgx_get_tables": (ctypes.c_int, [ctypes.c_void_p] * 3),
     "fgx_episode_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "fgx_selftest_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
-EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2",
-                   5: "k_episode_jl_pc"}
+EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2"}
 
 _LIB = None
 
@@ -107,7 +108,10 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fgx_abi_version() != FGX_ABI_VERSION:
+    abi = lib.fgx_abi_version()
+    # (FGX_LIB_ABI6=1: an experiment may load an ABI-6 build -- same config layout, single-counter
+    # inner_steps, which still sums right in the ABI-7 counter array)
+    if abi != FGX_ABI_VERSION and not (abi == 6 and os.environ.get("FGX_LIB") and os.environ.get("FGX_LIB_ABI6")):
         raise FgxError("libfgx ABI version mismatch")
     if path == LIB_PATH:   # build provenance: the in-tree library must match the in-tree sources
         from . import _build

@@ -20,6 +20,8 @@
 
 using namespace fgx;
 
+static_assert(kInnerSlots == FGX_INNER_SLOTS && kInnerStride == FGX_INNER_STRIDE, "inner-step counter layout");
+
 namespace {
 
 thread_local std::string g_err;
@@ -296,9 +298,30 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   return FGX_OK;
 }
 
+__global__ void k_selftest_sincos(const double* x, int64_t n, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s, c;
+  fgx_sincos(x[i], &s, &c);
+  out[4 * i] = s;
+  out[4 * i + 1] = c;
+  sincos_ocml(x[i], &s, &c);
+  out[4 * i + 2] = s;
+  out[4 * i + 3] = c;
+}
+
 extern "C" {
 
 const char* fgx_last_error(void) { return g_err.c_str(); }
+
+int fgx_selftest_sincos(const double* x, int64_t n, double* out, void* stream) {
+  if (!x || !out || n < 0) return fail(FGX_E_INVALID, "bad argument");
+  if (n == 0) return FGX_OK;
+  hipLaunchKernelGGL(k_selftest_sincos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n,
+                     out);
+  HIP_TRY(hipGetLastError());
+  return FGX_OK;
+}
 
 int fgx_abi_version(void) { return FGX_ABI_VERSION; }
 

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "fgx_rng.h"
+#include "fgx_trig.h"
 
 namespace fgx {
 
@@ -142,6 +143,16 @@ struct Outputs {
 #else
 #define FGX_STAMP(o, e, i) do { } while (0)
 #endif
+
+// The device inner-step counter (fgx_info.inner_steps, include/fgx.h): `sum` (the trajectory
+// lengths of this wave's envs, already reduced) goes to the wave's line of FGX_INNER_SLOTS partial
+// counters by one lane -- one device-scope atomic per wave, spread over the lines.
+constexpr int kInnerSlots = 128, kInnerStride = 16;   // = FGX_INNER_SLOTS / FGX_INNER_STRIDE (fgx_api.hip)
+__device__ __forceinline__ void count_inner(long long* base, long long sum, bool leader) {
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (leader && sum != 0)
+    atomicAdd((unsigned long long*)(base + (size_t)(w % kInnerSlots) * kInnerStride), (unsigned long long)sum);
+}
 
 // ------------------------------------------------------------------ wave reductions (all 64 lanes active)
 __device__ __forceinline__ int wave_min(int x) {
@@ -340,7 +351,7 @@ struct Env {
     for (int k = 0; k < NL; ++k) {
       ang = (k == 0) ? q[0] : ang + q[k];
       double sn, cs;
-      sincos(ang, &sn, &cs);
+      fgx_sincos(ang, &sn, &cs);
       c[k] = cs; s[k] = sn;
       x = (k == 0) ? cs : x + cs;
       y = (k == 0) ? sn : y + sn;
@@ -474,7 +485,7 @@ struct Env {
   // (q0 + 0.0 == q0: q0 is never -0), so one sincos serves all links; the running sums are fk()'s
   __device__ __forceinline__ void fk_fresh() {
     double sn, cs;
-    sincos(q[0], &sn, &cs);
+    fgx_sincos(q[0], &sn, &cs);
     double x = 0.0, y = 0.0;
     jx[0] = 0.0; jy[0] = 0.0;
 #pragma unroll

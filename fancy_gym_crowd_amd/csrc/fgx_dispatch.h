@@ -43,14 +43,7 @@ namespace fgx {
 //    its exchange rows stopped conflicting on LDS banks).
 // k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
 // wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_JL_PC = 5 };
-
-// k_episode_jl's producer / consumer form (ProMP, 5 links, 5 basis functions): FGX_JL_PC=1 / 0 forces
-// it on / off (A/B); the default follows the measured table (fgx_jl.h)
-inline bool jl_pc_enabled() {
-  if (const char* v = std::getenv("FGX_JL_PC")) return std::strcmp(v, "0") != 0;
-  return false;
-}
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -80,17 +73,16 @@ inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env
                         !c.sched_state && c.T <= 256 && c.max_steps <= 200 && !per_env_plans && !c.learn_tau &&
                         !c.learn_delay && (c.nl == 2 || c.nl == 5);
   if (!eligible) return classic_choice(c, log);
-  const int jl = (mp == MP_PROMP && c.nl == 5 && c.nb == 5 && jl_pc_enabled()) ? EK_JL_PC : EK_JL;
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
     if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "w2") == 0) return classic_choice(c, log);
     if (std::strcmp(v, "jp") == 0) return EK_JP;
     if (std::strcmp(v, "ws") == 0) return EK_WS;
-    if (std::strcmp(v, "jl") == 0) return jl;
+    if (std::strcmp(v, "jl") == 0) return EK_JL;
   }
   const int64_t R = round_envs(), tail = c.N % R;
   if (c.nl == 2) return EK_JL;
-  if (4 * c.N <= 3 * R) return jl;
-  if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return jl;
+  if (4 * c.N <= 3 * R) return EK_JL;
+  if (!c.replan && c.N > R && tail != 0 && 2 * tail <= R) return EK_JL;
   return classic_choice(c, log);
 }
 
@@ -156,7 +148,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
-    if (k == EK_JL || k == EK_JL_PC) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
+    if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
   }
   if constexpr (ENV == ENV_SIMPLE && NL == 5) {
     if (classic_choice(c, log) == EK_CLASSIC_W2 &&

@@ -22,16 +22,6 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
   if (const char* v = std::getenv("FGX_JL_GW")) gw = std::max(1, std::min(S::G, std::atoi(v)));   // experiments
   const int64_t per_block = (int64_t)S::WAVES * gw;
   const unsigned blocks = (unsigned)((c.N + per_block - 1) / per_block);
-  if constexpr (MP == fgx::MP_PROMP && NL == 5 && NB == 5) {
-    if (fgx::jl_pc_enabled()) {   // producer / consumer wave pairs (k_episode_jl_pc)
-      using SP = fgx::JlShape<NL, true>;
-      hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB, true>), dim3(blocks), dim3(SP::THREADS), SP::lds_bytes(),
-                         stream, c, s, params, o, gw);
-      const hipError_t e = hipGetLastError();
-      if (e != hipSuccess) { err = std::string("k_episode_jl_pc launch: ") + hipGetErrorString(e); return -2; }
-      return 0;
-    }
-  }
   hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB>), dim3(blocks), dim3(S::THREADS), S::lds_bytes(), stream, c,
                      s, params, o, gw);
   const hipError_t e = hipGetLastError();

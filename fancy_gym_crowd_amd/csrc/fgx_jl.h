@@ -33,16 +33,13 @@
 
 namespace fgx {
 
-// PC: the producer / consumer form (k_episode_jl's joint waves paired with trajectory-producer waves)
-template <int NL, bool PC = false>
+template <int NL>
 struct JlShape {
   static constexpr int G = 64 / NL;             // envs per wave
-  static constexpr int WAVES = 4;               // joint (consumer) waves per workgroup
-  static constexpr int PW = PC ? WAVES : 0;     // trajectory-producer waves (wave w + WAVES pairs with w)
+  static constexpr int WAVES = 4;               // waves per workgroup
   static constexpr int EPB = G * WAVES;         // envs per workgroup
   static constexpr int SPW = (8 + NL - 1) / NL; // pairwise slots owned per lane
-  static constexpr int RW = (EPB + 63) / 64;    // reset waves: one lane per env of the workgroup
-  static constexpr int THREADS = 64 * (WAVES + PW + RW);
+  static constexpr int THREADS = 64 * WAVES;
   // gathered f64 per env: A, B, tail (8 each), cfk, q, qd, then cos / sin of the cumulative angles
   // (FK) and of every q (observation), then the env's stored steps, plan count, flags and goal
   static constexpr int GX = 25 + 6 * NL;
@@ -56,32 +53,12 @@ struct JlShape {
   // (90 -> 40, the LDS footprint shrinks; the 4 idle lanes do not write), 2 links stride 65
   // (32 -> 16, conflict-free; the gather area is larger anyway).  Writes stay conflict-free.
   static constexpr int XS = (G * NL < 64) ? G * NL + 1 : 65;
-  // PC: per wave pair two trajectory chunk buffers (8 samples of pos / vel as 4 float4 per lane) and
-  // three progress counters, after the exchange rows
-  static constexpr size_t ex_bytes() { return (size_t)WAVES * 16 * XS * sizeof(double); }
-  static constexpr size_t tb_bytes() { return PC ? (size_t)WAVES * 2 * 4 * 64 * 16 : 0; }
   static constexpr size_t lds_bytes() {
-    const size_t ex = ex_bytes() + tb_bytes() + (PC ? WAVES * 4 * sizeof(int) : 0);
+    const size_t ex = (size_t)WAVES * 16 * XS * sizeof(double);
     const size_t ga = (size_t)GF * EPB * sizeof(double);
     return ex > ga ? ex : ga;
   }
 };
-
-// Progress counters of a producer / consumer wave pair (LDS, workgroup scope).  A counter only grows;
-// the waiting wave polls it with s_sleep between reads, bounded so that a broken protocol can never
-// hang the GPU (the pair's results would be garbage, the kernel still ends).
-__device__ __forceinline__ void pc_wait_ge(int* f, int target) {
-  for (int spin = 0; spin < (1 << 22); ++spin) {
-    const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (v >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void pc_set(int* f, int v, int lane) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's LDS writes land first
-  if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // orders this wave's LDS writes before its later reads (and reads before later writes): LDS
 // operations of one wave execute in order, so the compiler's ordering is all that is needed
@@ -91,75 +68,17 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The reset waves of k_episode_jl (waves WAVES .. WAVES + RW - 1 of the workgroup, one lane per env).
-// The VectorEnv auto-reset of an env that truncates in this BB step (SimpleReacher never
-// terminates: steps + L >= max_steps is known before the rollout) depends only on its PCG64 stream
-// and start angle, not on the episode, so these waves draw it -- the PCG64 draws, the goal's
-// rejection loops, the fresh arm's FK and observation, most of the epilogue's instructions -- at
-// kernel entry, concurrently with the joint lanes' chunks (a reset wave shares its SIMD with a
-// joint wave and takes the issue slots that lone wave leaves idle), and write the new observation
-// row at once.  The env state is stored after the second workgroup barrier: by then every read of
-// the state in this launch is done (the joint lanes read it in their prologue / NaN restart, the
-// return threads read only the LDS gather).  The barrier count matches the joint waves'.
-template <int NL, bool PC>
-__device__ __forceinline__ void jl_reset_wave(const DevCfg& c, const DevState& s, const Outputs& o, int gw, int rw,
-                                              int lane) {
-  using S = JlShape<NL, PC>;
-  constexpr int G = S::G, EPB = S::EPB;
-  const int rl = rw * 64 + lane;   // the env slot of this lane (slot = joint wave * G + env)
-  const int tw = rl / G, tg = rl - tw * G;
-  const int64_t er = (int64_t)blockIdx.x * (S::WAVES * gw) + tw * gw + tg;
-  bool do_reset = false;
-  if (o.autoreset && rl < EPB && tg < gw && er < c.N) {
-    JpSeg sr;
-    sr.init(c, s, er, true);
-    do_reset = sr.steps + sr.L >= c.max_steps;   // the segment ends in truncation
-  }
-  Env<NL> vr;
-  Pcg64 rg;
-  if (do_reset) {
-    rg = load_rng(s.rng, c.N, er);
-    if (!c.random_start) vr.sp = s.start[er];
-    vr.reset(c, rg, false, 0);
-    emit_obs(c, vr, c.return_context, o.obs + er * c.out_dim, nullptr, true);
-  }
-  if (PC) __syncthreads();   // 0: the pair counters are initialised
-  __syncthreads();   // 1: the joint waves are done with their chunks
-  __syncthreads();   // 2: the gather is written (no later read of the env state in this launch)
-  if (do_reset) {
-    store_rng(s.rng, c.N, er, rg);
-    if (c.random_start) s.start[er] = vr.sp;
-    store_env(c, s, er, vr, false);   // SimpleReacher: no hole / reward state
-    s.plans[er] = 0;
-  }
-  __syncthreads();   // 3
-}
-
-template <int MP, int NL, int NB, bool PC = false>
+template <int MP, int NL, int NB>
 // gw: envs per wave actually used (<= G; experiments, FGX_JL_GW); LDS slots keep the compile-time
-// stride G.  PC: waves WAVES .. 2 WAVES - 1 are trajectory producers (see k_episode_jl_pc below)
-__global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevState s, const float* __restrict__ params,
-                                                               Outputs o, int gw) {
-  using S = JlShape<NL, PC>;
+// stride G
+__global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const float* __restrict__ params, Outputs o,
+                                                    int gw) {
+  using S = JlShape<NL>;
   constexpr int G = S::G, EPB = S::EPB, SPW = S::SPW;
   constexpr int NBL = NB > 0 ? NB : 1;
   extern __shared__ double lds_jl[];
   const int lane = threadIdx.x & 63;
-  const int wall = threadIdx.x >> 6;
-  if (wall >= S::WAVES + S::PW) {   // (wave-uniform)
-    jl_reset_wave<NL, PC>(c, s, o, gw, wall - S::WAVES - S::PW, lane);
-    return;
-  }
-  const bool producer = PC && wall >= S::WAVES;
-  const int w = producer ? wall - S::WAVES : wall;   // the pair's joint-wave index (env mapping)
-  // PC pair state: trajectory buffers and counters P (chunks produced), R (chunks reduced by the
-  // producer), C (chunks consumed: a^2 rows written)
-  float4* tbuf = (float4*)((char*)lds_jl + S::ex_bytes()) + (size_t)w * 2 * 4 * 64;
-  int* pcf = (int*)((char*)lds_jl + S::ex_bytes() + S::tb_bytes()) + w * 4;
-  if constexpr (PC) {
-    if (!producer && lane == 0) { pcf[0] = 0; pcf[1] = 0; pcf[2] = 0; }
-    __syncthreads();   // 0
-  }
+  const int w = threadIdx.x >> 6;
   constexpr int XS = S::XS;
   double* ex = lds_jl + w * (16 * XS);  // this wave's two chunk buffers: a^2 of sample j at [j * XS + lane]
   const int g = lane / NL, d = lane - g * NL;
@@ -169,7 +88,7 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
   const bool valid = g < gw && e0 < N;
   const int64_t e = valid ? e0 : N - 1;   // clamped: loads stay in bounds, nothing is stored
   const uint64_t vmask = __ballot(valid);
-  const int64_t wst = ((int64_t)blockIdx.x * (S::WAVES + S::PW) + wall) * 64;   // diagnostics build: stamp slot
+  const int64_t wst = ((int64_t)blockIdx.x * S::WAVES + w) * 64;   // diagnostics build: stamp slot of this wave
   FGX_STAMP(o, wst, 6);
   FGX_STAMP(o, wst, 0);
 
@@ -482,118 +401,9 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
     if (kfk < 0x7fffffff) nf = min(nf, kfk / 8 + 1);
     return max(0, min(nf, nchunks));
   };
-  // ---- PC: the fast chunks split over the wave pair (k_episode_jl_pc below).  The producer evaluates
-  // the trajectory chunks 0 .. nf (ProMP column loads, the same operations as traj / traj_fast, the
-  // plan's last-sample velocity patched in) into the pair's two chunk buffers and reduces the a^2
-  // rows of chunks 0 .. nf - 2 into its copy of the pairwise slots; the consumer runs the PD / clip /
-  // Euler recurrence of chunks 0 .. nf - 1 from the buffers and writes the a^2 rows, then takes over
-  // the producer's generator state and slot sums and finishes as k_episode_jl does.
-  auto tb_put = [&](int j, const float* Pt, const float* Vt) __attribute__((always_inline)) {
-    float4* b = tbuf + (j & 1) * 4 * 64;
-    b[lane] = make_float4(Pt[0], Pt[1], Pt[2], Pt[3]);
-    b[64 + lane] = make_float4(Pt[4], Pt[5], Pt[6], Pt[7]);
-    b[128 + lane] = make_float4(Vt[0], Vt[1], Vt[2], Vt[3]);
-    b[192 + lane] = make_float4(Vt[4], Vt[5], Vt[6], Vt[7]);
-  };
-  auto tb_get = [&](int j, float* Pt, float* Vt) __attribute__((always_inline)) {
-    const float4* b = tbuf + (j & 1) * 4 * 64;
-    const float4 a0 = b[lane], a1 = b[64 + lane], a2 = b[128 + lane], a3 = b[192 + lane];
-    Pt[0] = a0.x; Pt[1] = a0.y; Pt[2] = a0.z; Pt[3] = a0.w; Pt[4] = a1.x; Pt[5] = a1.y; Pt[6] = a1.z; Pt[7] = a1.w;
-    Vt[0] = a2.x; Vt[1] = a2.y; Vt[2] = a2.z; Vt[3] = a2.w; Vt[4] = a3.x; Vt[5] = a3.y; Vt[6] = a3.z; Vt[7] = a3.w;
-  };
-  // hand-off record (in the buffer of chunk nf + 1): generator position / velocity, the slot sums
-  auto ho_put = [&](int nf) __attribute__((always_inline)) {
-    float* b = (float*)(tbuf + ((nf + 1) & 1) * 4 * 64) + lane * 16;
-    b[0] = tg.cur[0];
-    b[1] = tg.vprev[0];
-#pragma unroll
-    for (int sl = 0; sl < SPW; ++sl) {
-      ((double*)(b + 2))[3 * sl] = A[sl];
-      ((double*)(b + 2))[3 * sl + 1] = B[sl];
-      ((double*)(b + 2))[3 * sl + 2] = Tl[sl];
-    }
-  };
-  auto ho_get = [&](int nf) __attribute__((always_inline)) {
-    const float* b = (const float*)(tbuf + ((nf + 1) & 1) * 4 * 64) + lane * 16;
-    tg.cur[0] = b[0];
-    tg.vprev[0] = b[1];
-#pragma unroll
-    for (int sl = 0; sl < SPW; ++sl) {
-      A[sl] = ((const double*)(b + 2))[3 * sl];
-      B[sl] = ((const double*)(b + 2))[3 * sl + 1];
-      Tl[sl] = ((const double*)(b + 2))[3 * sl + 2];
-    }
-  };
-  auto pc_produce = [&](int nf) __attribute__((always_inline)) {
-    float Pt[8], Vt[8];
-    traj(0, Pt, Vt, std::false_type{}, std::true_type{});
-    tb_put(0, Pt, Vt);
-    pc_set(&pcf[0], 1, lane);
-    float vprevc = Vt[7];
-    for (int j = 1; j <= nf; ++j) {
-      Cols cl;
-      traj_load(8 * j, cl);
-      traj_fast(8 * j, cl, Pt, Vt);
-      if (__builtin_expect(j == cpch, 0)) {   // the plan's last sample: the previous velocity (Traj::at)
-        float prev = vprevc;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float vj = Vt[jj];
-          if (jj == ip) Vt[jj] = prev;
-          prev = vj;
-        }
-      }
-      vprevc = Vt[7];
-      if (j == nf) {
-        pc_wait_ge(&pcf[2], nf);   // chunk nf - 1 consumed: both buffers are free but chunk nf's
-        ho_put(nf);
-      } else {
-        pc_wait_ge(&pcf[2], j - 1);   // chunk j - 2 consumed: its buffer is free
-      }
-      tb_put(j, Pt, Vt);
-      pc_set(&pcf[0], j + 1, lane);
-      if (j <= nf - 1) {
-        pc_wait_ge(&pcf[2], j);   // chunk j - 1's a^2 rows are written
-        reduce(j - 1);
-        pc_set(&pcf[1], j, lane);
-      }
-    }
-  };
-  auto pc_consume = [&](int nf) __attribute__((always_inline)) {
-    for (int cc = 0; cc < nf; ++cc) {
-      pc_wait_ge(&pcf[0], cc + 1);                 // chunk cc's trajectory
-      if (cc >= 2) pc_wait_ge(&pcf[1], cc - 1);     // chunk cc - 2's rows reduced: its a^2 buffer is free
-      float Pc[8], Vc[8];
-      tb_get(cc, Pc, Vc);
-      dyn(8 * cc, Pc, Vc, sq, std::true_type{}, std::integral_constant<int, 2>{});   // NaN-free waves only
-      write_sq(cc, sq);
-      plast = Pc[7];
-      vlast = Vc[7];
-      pc_set(&pcf[2], cc + 1, lane);
-    }
-    pc_wait_ge(&pcf[0], nf + 1);   // chunk nf's trajectory and the hand-off record
-    tb_get(nf, P, V);
-    ho_get(nf);
-    wave_lds_sync();
-  };
   auto run = [&](auto sc, auto exact) __attribute__((always_inline)) {
     const int nchunks = (Lmax + 7) / 8;
     if (nchunks == 0) return;
-    if constexpr (PC && decltype(sc)::value && decltype(exact)::value == 0) {
-      const int nf = fast_count(nchunks);
-      if (nf > 0) {
-        if (producer) {
-          pc_produce(nf);
-          return;
-        }
-        pc_consume(nf);
-        if (8 * nf == Lmin) { posl = plast; vell = vlast; }
-        FGX_STAMP(o, wst, 2);
-        slow_range(nf, nchunks, sc, exact);
-        return;
-      }
-    }
-    if (producer) return;   // the pair does not take the split path: the joint wave runs it alone
     traj(0, P, V, std::false_type{}, sc);
     int ch = 0;
     if constexpr (decltype(sc)::value && decltype(exact)::value == 0) {
@@ -628,14 +438,6 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
   FGX_STAMP(o, wst, 1);
   if (s0_uni) run(std::true_type{}, std::integral_constant<int, 0>{});
   else run(std::false_type{}, std::integral_constant<int, 0>{});
-  if constexpr (PC) {
-    if (producer) {   // the joint wave of the pair finishes alone; the barriers of the gather
-      __syncthreads();   // 1
-      __syncthreads();   // 2
-      __syncthreads();   // 3
-      return;
-    }
-  }
   if (__builtin_expect((nanm & vmask) != 0, 0)) {   // a NaN control: np.clip semantics from the start
     wave_lds_sync();
     restart();
@@ -649,14 +451,23 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
   }
 
   FGX_STAMP(o, wst, 3);
-  if (o.inner_steps) {   // sum of trajectory lengths (joint 0 lanes): one atomic per wave
-    long long sum = (valid && d == 0) ? sg.L : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-    if (lane == 0 && sum != 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
-  }
   double gx = 0.0, gy = 0.0;   // the env's goal, for the return thread (FK reward, observation)
   if (d == 0) { gx = s.goal[e]; gy = s.goal[N + e]; }
+  // The VectorEnv auto-reset of a truncated env depends only on its PCG64 stream and start angle,
+  // not on the episode: when the workgroup has a second group of EPB threads (R0 = EPB rounded up to
+  // whole waves), those threads run the resets concurrently with the first group's returns and
+  // final observations.  Their inputs are loaded here, so that the loads land under the gather.
+  constexpr int R0 = (EPB + 63) / 64 * 64;
+  constexpr bool SPLIT = R0 + EPB <= 64 * S::WAVES;
+  const int t1 = (int)threadIdx.x - R0, tw1 = t1 / G, tg1 = t1 - tw1 * G;
+  const int64_t er = (int64_t)blockIdx.x * (S::WAVES * gw) + tw1 * gw + tg1;
+  const bool rgrp = SPLIT && o.autoreset && t1 >= 0 && t1 < EPB && tg1 < gw && er < N;
+  Pcg64 rg;
+  double rsp = 0.0;
+  if (rgrp) {
+    rg = load_rng(s.rng, N, er);
+    rsp = s.start[er];
+  }
   // ---- gather per env (SoA [field][EPB]): slot sums, the FK sample's control cost, joint state,
   // the env's segment words and goal
   __syncthreads();   // 1: every wave is done with its chunk rows (the gather area overlaps them)
@@ -693,8 +504,8 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
       ang = (k <= d) ? nx : ang;
     }
     double fs, fc, os_, oc;
-    sincos(ang, &fs, &fc);
-    sincos(q, &os_, &oc);
+    fgx_sincos(ang, &fs, &fc);
+    fgx_sincos(q, &os_, &oc);
     ga[(25 + 2 * NL + d) * EPB + slot] = fc;
     ga[(25 + 3 * NL + d) * EPB + slot] = fs;
     ga[(25 + 4 * NL + d) * EPB + slot] = oc;
@@ -702,13 +513,42 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
   }
   __syncthreads();   // 3
 
-  // ---- one thread per env: return and epilogue (threads t < EPB), from the LDS gather only.  The
-  // reset waves (jl_reset_wave) run the auto-reset of every truncating env.
+  // ---- the reset group: the auto-reset of every env whose segment ends in truncation (SimpleReacher
+  // never terminates); nothing in this launch reads the env state after the gather
+  FGX_STAMP(o, wst, 4);
+  if (rgrp) {
+    JpSeg sr;
+    sr.init_vals(c, (int)ga[(S::GX + 0) * EPB + t1], (uint32_t)ga[(S::GX + 2) * EPB + t1],
+                 (int)ga[(S::GX + 1) * EPB + t1], true);
+    if (sr.steps + sr.L >= c.max_steps) {
+      Env<NL> vr;
+      if (!c.random_start) vr.sp = rsp;
+      vr.reset(c, rg, false, 0);
+      store_rng(s.rng, N, er, rg);
+      if (c.random_start) s.start[er] = vr.sp;
+      emit_obs(c, vr, c.return_context, o.obs + er * c.out_dim, nullptr, true);
+      store_env(c, s, er, vr, false);   // SimpleReacher: no hole / reward state
+      s.plans[er] = 0;
+    }
+    FGX_STAMP(o, wst, 10);
+  }
+  // ---- one thread per env: return and epilogue (threads t < EPB), from the LDS gather only
   const int t = threadIdx.x;
   const int tw = t / G, tg_ = t - tw * G;   // slot t = tw * G + tg_
   const int64_t et = (int64_t)blockIdx.x * (S::WAVES * gw) + tw * gw + tg_;
   const bool tv = t < EPB && tg_ < gw && et < N;
-  FGX_STAMP(o, wst, 4);
+  if (o.inner_steps && (t >> 6) < (EPB + 63) / 64) {   // trajectory lengths: one atomic per wave of the group
+    long long sum = 0;
+    if (tv) {
+      JpSeg sq;
+      sq.init_vals(c, (int)ga[(S::GX + 0) * EPB + t], (uint32_t)ga[(S::GX + 2) * EPB + t],
+                   (int)ga[(S::GX + 1) * EPB + t], true);
+      sum = sq.L;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    count_inner(o.inner_steps, sum, lane == 0);
+  }
   if (!tv) {
     FGX_STAMP(o, wst, 5);
     FGX_STAMP(o, wst, 7);
@@ -754,7 +594,7 @@ __global__ __launch_bounds__(PC ? 640 : 384) void k_episode_jl(DevCfg c, DevStat
     if (j < ntail) res = res + ((fk_last && j == ntail - 1) ? r_fk : ga[(3 * j + 2) * EPB + t]);
   if (L > 128) res = PairwiseSum::comb(sa) + res;
   const bool trunc = v.steps >= c.max_steps;
-  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_, true);
+  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_, SPLIT);
   FGX_STAMP(o, wst, 5);
   FGX_STAMP(o, wst, 7);
 }

@@ -48,7 +48,7 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
       for (int k = 0; k < NL; ++k) {
         if (gcs) { cs[k] = gcs[k]; sn[k] = gsn[k]; }
         else if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
-        else sincos(v.q[k], &sn[k], &cs[k]);
+        else fgx_sincos(v.q[k], &sn[k], &cs[k]);
       }
     }
 #pragma unroll
@@ -172,9 +172,16 @@ struct Traj {
   // bit-identical to the scalar chain); an odd last joint rides in the low half of a pair whose
   // high half is zero.
   static constexpr bool PK = (MP == MP_PROMP) && NL >= 2;
+  // ProDMP with >= 2 joints: the two basis contractions (position, velocity) on joint pairs likewise
+#ifdef FGX_NO_PKD   // A/B builds only: the scalar chains
+  static constexpr bool PKD = false;
+#else
+  static constexpr bool PKD = (MP == MP_PRODMP) && NL >= 2;
+#endif
   static constexpr int NLP = (NL + 1) / 2;
-  float w[PK ? 1 : NL][K]; // ProMP (1 joint): w ; DMP: w' ; ProDMP: [w' (NBM slots), g', c1, c2]
+  float w[(PK || PKD) ? 1 : NL][K]; // ProMP (1 joint): w ; DMP: w' ; ProDMP (1 joint): [w' (NBM slots), g', c1, c2]
   f32x2 wp[PK ? NLP : 1][PK ? NBM : 1];   // ProMP (>= 2 joints): weights of joints (2p, 2p + 1)
+  f32x2 wq[PKD ? NLP : 1][PKD ? K : 1];   // ProDMP (>= 2 joints): [w', g', c1, c2] of joints (2p, 2p + 1)
   f32x2 cur2[PK ? NLP : 1], vprev2[PK ? NLP : 1];
   float g[NL];             // DMP goal
   float y[NL], z[NL];      // DMP state
@@ -191,6 +198,7 @@ struct Traj {
   // weight j of joint d (any layout)
   __device__ __forceinline__ float wt(int d, int j) const {
     if constexpr (PK) return (d & 1) ? wp[d >> 1][j].y : wp[d >> 1][j].x;
+    else if constexpr (PKD) return (d & 1) ? wq[d >> 1][j].y : wq[d >> 1][j].x;
     else return w[d][j];
   }
   __device__ __forceinline__ int nb() const { return NB ? NB : nbr; }
@@ -221,6 +229,19 @@ struct Traj {
     acc = __builtin_fmaf(h[NBM], wd[NBM], acc);
     acc = __builtin_fmaf(h[NBM + 1], wd[NBM + 1], acc);
     return __builtin_fmaf(h[NBM + 2], wd[NBM + 2], acc);
+  }
+  // the same chain on a joint pair
+  __device__ __forceinline__ f32x2 chain3_2(const float* h, const f32x2* wd) const {
+    f32x2 acc = chain2(h, wd);
+    acc = __builtin_elementwise_fma((f32x2)h[NBM], wd[NBM], acc);
+    acc = __builtin_elementwise_fma((f32x2)h[NBM + 1], wd[NBM + 1], acc);
+    return __builtin_elementwise_fma((f32x2)h[NBM + 2], wd[NBM + 2], acc);
+  }
+  __device__ __forceinline__ f32x2 div_tau2(f32x2 x) const {
+    if constexpr (DIVREF) return x / (f32x2)tau32;   // two IEEE divisions
+    const f32x2 q = x * rtau32;                       // div_rcp on the pair
+    const f32x2 e = __builtin_elementwise_fma(-q, (f32x2)tau32, x);
+    return __builtin_elementwise_fma(e, (f32x2)rtau32, q);
   }
 
   // params: this env's row of the [N, n_params] matrix; q0/qd0 the initial conditions
@@ -279,16 +300,26 @@ struct Traj {
       hv[NBM] = rb[2 * n + 1];
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
+        float wd[K];
 #pragma unroll
-        for (int j = 0; j < NBM; ++j) w[d][j] = (NB || j < n) ? params[d * (n + 1) + j] * c.ws32 : 0.0f;
-        w[d][NBM] = params[d * (n + 1) + n] * c.gs32;
+        for (int j = 0; j < NBM; ++j) wd[j] = (NB || j < n) ? params[d * (n + 1) + j] * c.ws32 : 0.0f;
+        wd[NBM] = params[d * (n + 1) + n] * c.gs32;
         // P, V = [basis, goal] . [w', g'] (chain over nb + 1 entries)
-        float P = __builtin_fmaf(hp[NBM], w[d][NBM], chain(hp, w[d]));
-        float V = __builtin_fmaf(hv[NBM], w[d][NBM], chain(hv, w[d]));
+        float P = __builtin_fmaf(hp[NBM], wd[NBM], chain(hp, wd));
+        float V = __builtin_fmaf(hv[NBM], wd[NBM], chain(hv, wd));
         const float A = (float)q0[d] - P;
         const float B = (float)qd0[d] * tau32 - V;
-        w[d][NBM + 1] = (dy2 * A - y2 * B) / det;
-        w[d][NBM + 2] = (y1 * B - dy1 * A) / det;
+        wd[NBM + 1] = (dy2 * A - y2 * B) / det;
+        wd[NBM + 2] = (y1 * B - dy1 * A) / det;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          if constexpr (PKD) {
+            if (d & 1) wq[d >> 1][j].y = wd[j];
+            else wq[d >> 1][j] = (f32x2){wd[j], 0.0f};   // (an odd last joint: zero high half)
+          } else {
+            w[d][j] = wd[j];
+          }
+        }
       }
     }
   }
@@ -368,10 +399,21 @@ struct Traj {
       hp[NBM] = row[n]; hv[NBM] = row[2 * n + 1];
       hp[NBM + 1] = row[2 * n + 2]; hp[NBM + 2] = row[2 * n + 3];
       hv[NBM + 1] = row[2 * n + 4]; hv[NBM + 2] = row[2 * n + 5];
+      if constexpr (PKD) {
 #pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        pos[d] = chain3(hp, w[d]);
-        vel[d] = div_tau(chain3(hv, w[d]));
+        for (int p = 0; p < NLP; ++p) {
+          const f32x2 ps = chain3_2(hp, wq[p]);
+          const f32x2 vs = div_tau2(chain3_2(hv, wq[p]));
+          pos[2 * p] = ps.x;
+          vel[2 * p] = vs.x;
+          if (2 * p + 1 < NL) { pos[2 * p + 1] = ps.y; vel[2 * p + 1] = vs.y; }
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < NL; ++d) {
+          pos[d] = chain3(hp, w[d]);
+          vel[d] = div_tau(chain3(hv, w[d]));
+        }
       }
     }
   }
@@ -537,7 +579,7 @@ __device__ inline double obs_entry(const DevCfg& c, const Env<NL>& v, int idx) {
 #pragma unroll
     for (int j = 0; j < NL; ++j) qk = (j == k) ? v.q[j] : qk;
     double sn, cs;
-    sincos(qk, &sn, &cs);
+    fgx_sincos(qk, &sn, &cs);
     return (double)(float)(idx < NL ? cs : sn);
   }
   if (idx < 3 * NL) {
@@ -615,14 +657,14 @@ __device__ __forceinline__ void episode_epilogue(const DevCfg& c, const DevState
   o.term[e] = term;
   o.trunc[e] = trunc;
   o.tlen[e] = L;
-  if (count && o.inner_steps) {   // (count = false: the caller adds L to inner_steps itself)   // wave-reduce the trajectory lengths, one atomic per (full) wave
-    if (__ballot(1) == ~0ull) {
+  if (count && o.inner_steps) {   // (count = false: the caller adds L to inner_steps itself)
+    if (__ballot(1) == ~0ull) {   // wave-reduce the trajectory lengths: one atomic per (full) wave
       long long sum = L;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-      if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)sum);
+      count_inner(o.inner_steps, sum, (threadIdx.x & 63) == 0);
     } else {
-      atomicAdd((unsigned long long*)o.inner_steps, (unsigned long long)L);
+      count_inner(o.inner_steps, L, true);
     }
   }
   float* ob = o.obs + e * c.out_dim;

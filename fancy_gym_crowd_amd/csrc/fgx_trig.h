@@ -1,0 +1,81 @@
+// fgx_trig.h — f64 sin / cos for the kernels: the ocml algorithm (ROCm device libs,
+// __ocml_sincos_f64) restated operation for operation, so every result is bit-identical to
+// sincos(); only the argument reduction differs in *how* it is reached.  ocml reduces |x| < 2^30
+// with a three-part Cody-Waite step and larger |x| with a Payne-Hanek step (v_trig_preop_f64), and
+// the compiler, both being side-effect free, if-converts the two into straight-line code: every
+// sincos() call then executes the large-argument reduction as well (~100 of its ~155 VALU
+// instructions, tools: isa_blocks.py on a one-call kernel).  Here the small path runs inline and
+// |x| >= 2^30, inf and NaN take a real branch to ocml.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace fgx {
+
+static __device__ __attribute__((noinline)) void sincos_ocml(double x, double* s, double* c) { ::sincos(x, s, c); }
+
+__device__ __forceinline__ double bits_f64(unsigned long long u) { return __longlong_as_double((long long)u); }
+
+__device__ __forceinline__ void fgx_sincos(double x, double* sp, double* cp) {
+#ifdef FGX_OCML_SINCOS   // A/B builds only: the library call
+  ::sincos(x, sp, cp);
+  return;
+#endif
+  const double ax = __builtin_fabs(x);
+  if (__builtin_expect(!(ax < 0x1p30), 0)) {   // (and inf / NaN)
+    sincos_ocml(x, sp, cp);
+    return;
+  }
+  // __ocmlpriv_trigredsmall_f64(ax): r = hi + lo, quadrant i
+  const double k = __builtin_rint(ax * bits_f64(0x3FE45F306DC9C883ull));
+  const double r4 = __builtin_fma(k, bits_f64(0xBFF921FB54442D18ull), ax);
+  const double r5 = __builtin_fma(k, bits_f64(0xBC91A62633145C00ull), r4);
+  const double r6 = k * bits_f64(0x3C91A62633145C00ull);
+  const double r8 = __builtin_fma(k, bits_f64(0x3C91A62633145C00ull), -r6);
+  const double r9 = r4 - r6;
+  const double r10 = r4 - r9;
+  const double r11 = r10 - r6;
+  const double r12 = r9 - r5;
+  const double r13 = r12 + r11;
+  const double r14 = r13 - r8;
+  const double r15 = __builtin_fma(k, bits_f64(0xB97B839A252049C0ull), r14);
+  const double hi = r5 + r15;
+  const double r17 = hi - r5;
+  const double lo = r15 - r17;
+  const int i = ((int)k) & 3;
+  // __ocmlpriv_sincosred2_f64(hi, lo)
+  const double x2 = hi * hi;
+  const double h = x2 * 0.5;
+  const double c5 = 1.0 - h;
+  const double c6 = 1.0 - c5;
+  const double c7 = c6 - h;
+  const double x4 = x2 * x2;
+  double pc = __builtin_fma(x2, bits_f64(0xBDA907DB46CC5E42ull), bits_f64(0x3E21EEB69037AB78ull));
+  pc = __builtin_fma(x2, pc, bits_f64(0xBE927E4FA17F65F6ull));
+  pc = __builtin_fma(x2, pc, bits_f64(0x3EFA01A019F4EC90ull));
+  pc = __builtin_fma(x2, pc, bits_f64(0xBF56C16C16C16967ull));
+  pc = __builtin_fma(x2, pc, bits_f64(0x3FA5555555555555ull));
+  const double c15 = __builtin_fma(hi, -lo, c7);
+  const double c16 = __builtin_fma(x4, pc, c15);
+  const double cr = c5 + c16;
+  double ps = __builtin_fma(x2, bits_f64(0x3DE5E0B2F9A43BB8ull), bits_f64(0xBE5AE600B42FDFA7ull));
+  ps = __builtin_fma(x2, ps, bits_f64(0x3EC71DE3796CDE01ull));
+  ps = __builtin_fma(x2, ps, bits_f64(0xBF2A01A019E83E5Cull));
+  ps = __builtin_fma(x2, ps, bits_f64(0x3F81111111110BB3ull));
+  const double s23 = hi * -x2;
+  const double s25 = __builtin_fma(s23, ps, lo * 0.5);
+  const double s26 = __builtin_fma(x2, s25, -lo);
+  const double s27 = __builtin_fma(s23, bits_f64(0xBFC5555555555555ull), s26);
+  const double sr = hi - s27;
+  // __ocml_sincos_f64: quadrant selection and signs
+  const unsigned flip = i > 1 ? 0x80000000u : 0u;
+  const bool even = (i & 1) == 0;
+  const double sm = even ? sr : cr;
+  const double cm = even ? cr : -sr;
+  const unsigned xs = (unsigned)((unsigned long long)__double_as_longlong(x) >> 32) & 0x80000000u;
+  const unsigned long long sb = (unsigned long long)__double_as_longlong(sm);
+  const unsigned long long cb = (unsigned long long)__double_as_longlong(cm);
+  *sp = __longlong_as_double((long long)(sb ^ ((unsigned long long)(xs ^ flip) << 32)));
+  *cp = __longlong_as_double((long long)(cb ^ ((unsigned long long)flip << 32)));
+}
+
+}  // namespace fgx

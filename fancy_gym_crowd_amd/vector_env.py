@@ -345,7 +345,8 @@ class BlackBoxVectorEnv:
     # ------------------------------------------------------------------ fast path (bench)
     def step_into(self, actions, obs, ret, te, tr, tl, fobs=None, inner_steps=None):
         """Allocation-free BB step into preallocated buffers (no argument checks; for benchmarks).
-        inner_steps: optional int64 [1] device counter += sum of trajectory lengths."""
+        inner_steps: optional zero-initialised int64 [_lib.INNER_STEPS_LEN] device partial counters
+        (new_inner_steps() allocates them): their sum += the sum of trajectory lengths."""
         _order_check(self)
         info = None
         if inner_steps is not None:
@@ -357,6 +358,10 @@ class BlackBoxVectorEnv:
                                ctypes.c_void_p(tr.data_ptr()), ctypes.c_void_p(tl.data_ptr()),
                                ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, info,
                                int(self.autoreset), self._eng.stream())
+
+    def new_inner_steps(self):
+        """Zeroed device partial counters for step_into(inner_steps=...); total = .sum()."""
+        return torch.zeros(_lib.INNER_STEPS_LEN, dtype=torch.int64, device=self.device)
 
     # ------------------------------------------------------------------ state / tables
     def get_state(self):

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 6
+#define FGX_ABI_VERSION 7
 
 /* error codes */
 #define FGX_OK 0
@@ -188,8 +188,17 @@ typedef struct fgx_info {
   double* end_effector;  /* [T, N, 2] HoleReacher / ViaPointReacher info                   */
   double* reward_dist;   /* [T, N]  SimpleReacher info                                     */
   double* reward_ctrl;   /* [T, N]  SimpleReacher info                                     */
-  int64_t* inner_steps;  /* [1] += sum of trajectory_length over all envs (device counter)   */
+  int64_t* inner_steps;  /* [FGX_INNER_STEPS_LEN] zero-initialised partial counters: their sum  */
+                         /* += the sum of trajectory_length over all envs (ABI 7; one device   */
+                         /* atomic per wave / workgroup, spread over FGX_INNER_SLOTS lines)     */
 } fgx_info;
+
+/* fgx_info.inner_steps: FGX_INNER_SLOTS counters, FGX_INNER_STRIDE int64 apart (one 128-B line each):
+ * a single counter serialised one device-scope atomic per wave (-6% on the 65536-env metric
+ * kernel, profiles/r03_count_ab.jsonl) */
+#define FGX_INNER_SLOTS 128
+#define FGX_INNER_STRIDE 16
+#define FGX_INNER_STEPS_LEN (FGX_INNER_SLOTS * FGX_INNER_STRIDE)
 
 const char* fgx_last_error(void);
 int fgx_abi_version(void);
@@ -253,6 +262,11 @@ int fgx_get_tables(void* handle, float* out, void* stream);
  * k_episode, as it does for a config with valid_flags).  All five give bit-identical results; the
  * choice follows measured speed (fgx_dispatch.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
+
+/* Diagnostics (tests): for x[0..n) (device f64), out[4 n] = {sin, cos} of the kernels' sincos
+ * (fgx_trig.h, the ocml algorithm with its small-argument reduction inlined) followed by {sin, cos}
+ * of the ocml library call, so a test can compare them bit for bit. */
+int fgx_selftest_sincos(const double* x, int64_t n, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -66,3 +66,28 @@ def test_single_env_matches_vector_env():
 
 def te_(t):
     return t[0].item()
+
+
+def test_kernel_sincos_bit_equals_ocml():
+    """fgx_trig.h's sincos (the ocml algorithm, small-argument reduction inlined) equals the ocml
+    library call bit for bit over random, near-multiple-of-pi/2, huge and special arguments."""
+    import ctypes
+    import numpy as np
+    from fancy_gym_crowd_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    k = np.arange(-2000, 2000, dtype=np.float64)
+    xs = np.concatenate([
+        rng.uniform(-7, 7, 400000), rng.uniform(-1e4, 1e4, 200000), rng.uniform(-1e9, 1e9, 50000),
+        rng.standard_normal(100000) * 1e-6, k * (np.pi / 2), np.nextafter(k * (np.pi / 2), np.inf),
+        np.nextafter(k * (np.pi / 4), -np.inf), np.array([0.0, -0.0, 5e-324, -5e-324, 2.0 ** 30, -(2.0 ** 30),
+                                                          np.nextafter(2.0 ** 30, 0), 1e300, -1e300, np.inf,
+                                                          -np.inf, np.nan, np.pi / 4, 3 * np.pi / 4])])
+    x = torch.from_numpy(xs).to(DEV)
+    out = torch.empty(4 * len(xs), dtype=torch.float64, device=DEV)
+    assert lib.fgx_selftest_sincos(ctypes.c_void_p(x.data_ptr()), len(xs), ctypes.c_void_p(out.data_ptr()),
+                                   None) == 0
+    torch.cuda.synchronize()
+    o = np_(out).reshape(-1, 4).view(np.int64)
+    np.testing.assert_array_equal(o[:, 0], o[:, 2])
+    np.testing.assert_array_equal(o[:, 1], o[:, 3])

@@ -99,13 +99,14 @@ def test_jl_vs_oracle_desynchronised():
             os.environ["FGX_EPISODE_KERNEL"] = old
 
 
-def test_jl_inner_steps_counter():
-    """step_into's device counter of inner steps (one atomic per wave in k_episode_jl) equals the
-    sum of trajectory lengths."""
+@pytest.mark.parametrize("kern", ["jl", "classic", "jp", "ws"])
+def test_jl_inner_steps_counter(kern):
+    """step_into's device inner-step counters (FGX_INNER_SLOTS partial counters, one atomic per wave
+    or workgroup, include/fgx.h) sum to the sum of trajectory lengths, for every episode kernel."""
     import os
     env_id, N = "fancy_ProMP/LongSimpleReacher-v0", 1000
     old = os.environ.get("FGX_EPISODE_KERNEL")
-    os.environ["FGX_EPISODE_KERNEL"] = "jl"
+    os.environ["FGX_EPISODE_KERNEL"] = kern
     try:
         env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
         env.reset(seed=1)
@@ -116,10 +117,18 @@ def test_jl_inner_steps_counter():
         te = torch.empty(N, dtype=torch.uint8, device=DEV)
         tr = torch.empty(N, dtype=torch.uint8, device=DEV)
         tl = torch.empty(N, dtype=torch.int32, device=DEV)
-        acc = torch.zeros(1, dtype=torch.int64, device=DEV)
+        acc = env.new_inner_steps()
         env.step_into(params, obs, ret, te, tr, tl, None, inner_steps=acc)
+        env.step_into(params, obs, ret, te, tr, tl, None, inner_steps=acc)   # accumulates
         torch.cuda.synchronize()
-        assert int(acc.item()) == int(tl.sum().item())
+        assert acc.numel() == 128 * 16 and int((acc != 0).sum()) > 1   # spread over the lines
+        env.reset(seed=1)
+        env.set_state(steps=(np.arange(N) % 200).astype(np.int32))
+        tot = 0
+        for _ in range(2):
+            env.step_into(params, obs, ret, te, tr, tl, None)
+            tot += int(tl.sum().item())
+        assert int(acc.sum().item()) == tot
     finally:
         if old is None:
             os.environ.pop("FGX_EPISODE_KERNEL", None)

@@ -24,8 +24,8 @@ def np_(t):
 
 
 def kernel_is(got, want):
-    """episode kernel name check; k_episode_jl_pc is k_episode_jl's producer / consumer form"""
-    return got == want or (want == "k_episode_jl" and got == "k_episode_jl_pc")
+    """episode kernel name check (env.episode_kernel(), fgx_dispatch.h)"""
+    return got == want
 
 
 def close(a, b, rtol=RTOL, atol=1e-6):

@@ -52,12 +52,12 @@ def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
     te = torch.empty(N, dtype=torch.uint8, device=dev)
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     tl = torch.empty(N, dtype=torch.int32, device=dev)
-    acc = torch.zeros(1, dtype=torch.int64, device=dev)
+    acc = env.new_inner_steps()
     t = timed(lambda: env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc), reps=reps)
     acc.zero_()
     env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
     torch.cuda.synchronize()
-    inner = int(acc.item())
+    inner = int(acc.sum().item())
     print(json.dumps(dict(kernel=env.episode_kernel(), config=label or env_id, envs=N, kernel_us=t * 1e6,
                           inner_steps_per_call=inner, inner_steps_per_s=inner / t,
                           mean_traj_len=inner / N)), flush=True)

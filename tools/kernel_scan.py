@@ -37,16 +37,17 @@ for N in sizes:
         te = torch.empty(N, dtype=torch.uint8, device=dev)
         tr = torch.empty(N, dtype=torch.uint8, device=dev)
         tl = torch.empty(N, dtype=torch.int32, device=dev)
-        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+        acc = env.new_inner_steps()
+        cnt = None if os.environ.get("SCAN_NO_COUNT") else acc   # the device inner-step counter (atomics)
         stream = torch.cuda.Stream(dev)
         with torch.cuda.stream(stream):
             for _ in range(3):
-                env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+                env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=cnt)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream):
                 for _ in range(reps):
-                    env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+                    env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=cnt)
             torch.cuda.synchronize()
             best = None
             for _ in range(3):
@@ -58,8 +59,9 @@ for N in sizes:
                 torch.cuda.synchronize()
                 t = e0.elapsed_time(e1) * 1e3 / reps
                 best = t if best is None else min(best, t)
-        inner = int(acc.item()) / reps
+        inner = int(acc.sum().item()) / reps if cnt is not None else float(tl.sum().item())
         print(json.dumps(dict(env=env_id, envs=N, forced=kname, kernel=got, us_per_bb_step=round(best, 2),
+                              counter=cnt is not None,
                               inner_steps_per_s=inner / (best * 1e-6), ret0=float(ret[0]))), flush=True)
         del g, env
         torch.cuda.synchronize()
