@@ -25,14 +25,15 @@ namespace fgx {
 // q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
 // fk0: FK is current for q (k_episode's epilogue), so cos / sin of q[0] are c[0] / s[0].
 // gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
+// s1: element stride of d1 (the per-step observations are component-major, [T, obs, N])
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
                                          bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
-                                         const double* gsn = nullptr) {
+                                         const double* gsn = nullptr, int64_t s1 = 1) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
-    if (d1) d1[p] = x;
+    if (d1) d1[p * s1] = x;
     if (d2) d2[p] = x;
     ++p;
   };
@@ -163,7 +164,10 @@ __global__ __launch_bounds__(256) void k_reset(DevCfg c, DevState s, const uint6
 // shortcut div_rcp is not verified) instead of div_rcp.
 constexpr int kGenBasis = 12;
 
-template <int MP, int NL, int NB, bool DIVREF = false>
+// PAIRS: the ProDMP joint-pair contraction (PKD) is allowed (k_episode takes it for SimpleReacher:
+// -5% at 65536 envs; the register-bound HoleReacher body measured +2% with it,
+// profiles/r03_ab_s4.jsonl)
+template <int MP, int NL, int NB, bool DIVREF = false, bool PAIRS = true>
 struct Traj {
   static constexpr int NBM = NB ? NB : kGenBasis;           // weight slots per dof
   static constexpr int K = (MP == MP_PRODMP) ? NBM + 3 : NBM;
@@ -176,7 +180,7 @@ struct Traj {
 #ifdef FGX_NO_PKD   // A/B builds only: the scalar chains
   static constexpr bool PKD = false;
 #else
-  static constexpr bool PKD = (MP == MP_PRODMP) && NL >= 2;
+  static constexpr bool PKD = PAIRS && (MP == MP_PRODMP) && NL >= 2;
 #endif
   static constexpr int NLP = (NL + 1) / 2;
   float w[(PK || PKD) ? 1 : NL][K]; // ProMP (1 joint): w ; DMP: w' ; ProDMP (1 joint): [w' (NBM slots), g', c1, c2]
@@ -780,7 +784,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     ic_q[k] = has_cond ? (double)s.cond[k * N + e] : v.q[k];
     ic_qd[k] = has_cond ? (double)s.cond[(NL + k) * N + e] : v.qd[k];
   }
-  Traj<(MP == MP_GIVEN ? MP_NONE : MP), NL, NB> tg;
+  Traj<(MP == MP_GIVEN ? MP_NONE : MP), NL, NB, false, ENV == ENV_SIMPLE> tg;
   if (MP != MP_GIVEN) tg.init(c, params + e * c.n_params, lds_tab, s0, ic_q, ic_qd);
 
   plans += 1;
@@ -802,18 +806,19 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     const float fnan = __builtin_nanf("");
     float pp[NL], pv[NL];
     for (int kk = L; kk < c.T; ++kk) {
-      const int64_t ek = (int64_t)kk * N + e;
+      const int64_t ek = (int64_t)kk * N + e;        // [T, N] arrays
+      const int64_t ed = (int64_t)kk * NL * N + e;   // [T, dof, N] arrays: component d at ed + d N
       if (o.positions && MP != MP_GIVEN) {
         gen.at(c, kk, pp, pv);
-        for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pp[d]; o.velocities[ek * NL + d] = pv[d]; }
+        for (int d = 0; d < NL; ++d) { o.positions[ed + d * N] = pp[d]; o.velocities[ed + d * N] = pv[d]; }
       }
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = dnan;
+        for (int d = 0; d < NL; ++d) o.step_actions[ed + d * N] = dnan;
       if (o.step_rewards) o.step_rewards[ek] = dnan;
       if (o.step_obs)
-        for (int q = 0; q < c.full_dim; ++q) o.step_obs[ek * c.full_dim + q] = fnan;
+        for (int q = 0; q < c.full_dim; ++q) o.step_obs[((int64_t)kk * c.full_dim + q) * N + e] = fnan;
       if (o.is_collided) { o.is_collided[ek] = 0; o.is_success[ek] = 0; }
-      if (o.end_effector) { o.end_effector[ek * 2] = dnan; o.end_effector[ek * 2 + 1] = dnan; }
+      if (o.end_effector) { o.end_effector[2 * kk * N + e] = dnan; o.end_effector[(2 * kk + 1) * N + e] = dnan; }
       if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
     }
   };
@@ -912,16 +917,21 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     }
     // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
     if (LOG) {
-      const int64_t ek = (int64_t)k * N + e;   // info arrays are time-major [T, N, ...]: coalesced
+      // the info arrays are time- and component-major ([T, N] / [T, X, N]): every store of a wave
+      // covers 64 consecutive envs
+      const int64_t ek = (int64_t)k * N + e;
+      const int64_t ed = (int64_t)k * NL * N + e;
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) o.step_actions[ek * NL + d] = a[d];
+        for (int d = 0; d < NL; ++d) o.step_actions[ed + d * N] = a[d];
       if (o.positions && MP != MP_GIVEN)
-        for (int d = 0; d < NL; ++d) { o.positions[ek * NL + d] = pos[d]; o.velocities[ek * NL + d] = vel[d]; }
+        for (int d = 0; d < NL; ++d) { o.positions[ed + d * N] = pos[d]; o.velocities[ed + d * N] = vel[d]; }
       if (o.step_rewards) o.step_rewards[ek] = r.reward;
-      if (o.step_obs) emit_obs(c, v, false, o.step_obs + ek * c.full_dim, nullptr);
+      // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
+      if (o.step_obs) emit_obs(c, v, false, o.step_obs + (int64_t)k * c.full_dim * N + e, nullptr, false, true,
+                               nullptr, nullptr, N);
       if (ENV != ENV_SIMPLE) {
         if (o.is_collided) { o.is_collided[ek] = r.coll; o.is_success[ek] = r.success; }
-        if (o.end_effector) { o.end_effector[ek * 2] = v.jx[NL]; o.end_effector[ek * 2 + 1] = v.jy[NL]; }
+        if (o.end_effector) { o.end_effector[2 * k * N + e] = v.jx[NL]; o.end_effector[(2 * k + 1) * N + e] = v.jy[NL]; }
       } else if (o.reward_dist) {
         o.reward_dist[ek] = r.rdist;
         o.reward_ctrl[ek] = r.rctrl;

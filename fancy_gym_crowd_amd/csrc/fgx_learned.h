@@ -67,20 +67,20 @@ __global__ __launch_bounds__(256) void k_traj_env(DevCfg c, DevState s, const fl
       dpos[(e * c.T + k) * NL + d] = pos[d];
       dvel[(e * c.T + k) * NL + d] = vel[d];
     }
-    if (info_pos) {   // info['positions'/'velocities'], time-major [T, N, dof]
+    if (info_pos) {   // info['positions'/'velocities'], time- and component-major [T, dof, N]
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        info_pos[((int64_t)k * N + e) * NL + d] = pos[d];
-        info_vel[((int64_t)k * N + e) * NL + d] = vel[d];
+        info_pos[((int64_t)k * NL + d) * N + e] = pos[d];
+        info_vel[((int64_t)k * NL + d) * N + e] = vel[d];
       }
     }
   }
-  if (info_pos)   // the plan ends at T_e: NaN beyond (info arrays are [T, N, dof])
+  if (info_pos)   // the plan ends at T_e: NaN beyond (info arrays are [T, dof, N])
     for (int k = Te; k < c.T; ++k)
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
-        info_pos[((int64_t)k * N + e) * NL + d] = __builtin_nanf("");
-        info_vel[((int64_t)k * N + e) * NL + d] = __builtin_nanf("");
+        info_pos[((int64_t)k * NL + d) * N + e] = __builtin_nanf("");
+        info_vel[((int64_t)k * NL + d) * N + e] = __builtin_nanf("");
       }
   if (plan_len) plan_len[e] = Te;
 }

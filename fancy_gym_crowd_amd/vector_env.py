@@ -211,9 +211,9 @@ class BlackBoxVectorEnv:
 
     def _info_buffers(self):
         """Per-step info arrays of the info level (module docstring).  The device writes them
-        time-major ([T, N, ...], coalesced across envs, include/fgx.h fgx_info); the caller sees
-        [N, T, ...] transposed views.  A reward_aggregation other than sum / mean also needs
-        step_rewards."""
+        time- and component-major ([T, N] and [T, X, N], so that every wave store covers 64
+        consecutive envs, include/fgx.h fgx_info); the caller sees [N, T, ...] views.  A
+        reward_aggregation other than sum / mean also needs step_rewards."""
         generic_agg = self._needs_step_rewards()
         if self.info_level == 0 and not generic_agg:
             return None, {}
@@ -223,8 +223,8 @@ class BlackBoxVectorEnv:
         raw = {}
         info = _lib.FgxInfo()
         if self.info_level >= 2:
-            raw.update(positions=e(T, N, n), velocities=e(T, N, n), step_actions=e(T, N, n, dt=torch.float64),
-                       step_observations=e(T, N, self.full_dim))
+            raw.update(positions=e(T, n, N), velocities=e(T, n, N), step_actions=e(T, n, N, dt=torch.float64),
+                       step_observations=e(T, self.full_dim, N))
             info.positions, info.velocities = raw["positions"].data_ptr(), raw["velocities"].data_ptr()
             info.step_actions, info.step_obs = raw["step_actions"].data_ptr(), raw["step_observations"].data_ptr()
         if self.info_level >= 2 or generic_agg:
@@ -234,14 +234,14 @@ class BlackBoxVectorEnv:
             if self.meta["kind"] in ("hole", "via"):
                 raw["is_collided"] = e(T, N, dt=torch.uint8)
                 raw["is_success"] = e(T, N, dt=torch.uint8)
-                raw["end_effector"] = e(T, N, 2, dt=torch.float64)
+                raw["end_effector"] = e(T, 2, N, dt=torch.float64)
                 info.is_collided, info.is_success = raw["is_collided"].data_ptr(), raw["is_success"].data_ptr()
                 info.end_effector = raw["end_effector"].data_ptr()
             else:
                 raw["reward_dist"] = e(T, N, dt=torch.float64)
                 raw["reward_ctrl"] = e(T, N, dt=torch.float64)
                 info.reward_dist, info.reward_ctrl = raw["reward_dist"].data_ptr(), raw["reward_ctrl"].data_ptr()
-        return info, {k: v.transpose(0, 1) for k, v in raw.items()}
+        return info, {k: (v.transpose(0, 1) if v.dim() == 2 else v.permute(2, 0, 1)) for k, v in raw.items()}
 
     def _check_actions(self, actions):
         a = torch.as_tensor(actions, device=self.device)

@@ -175,17 +175,18 @@ typedef struct fgx_dims {
 /* Optional per-step outputs of fgx_step / fgx_step_traj (black_box_wrapper.py:185-249,
  * verbose >= 2).  Any pointer may be NULL.  Rows after trajectory_length are set to NaN (0 for the
  * u8 flags); positions / velocities hold the whole plan (NaN after a learned plan length).
- * The arrays are TIME-MAJOR, [T, N, ...] (sample k of env e at row k*N + e), so that the
- * per-step writes of neighbouring envs are coalesced; [N, T, ...] is a transposed view. */
+ * The arrays are TIME- AND COMPONENT-MAJOR (ABI 7): [T, N] (sample k of env e at k*N + e) and
+ * [T, X, N] (component x at (k*X + x)*N + e), so that a wave's per-step stores cover consecutive
+ * envs; [N, T] / [N, T, X] are transposed / permuted views. */
 typedef struct fgx_info {
-  float* positions;      /* [T, N, dof]  desired positions                                 */
-  float* velocities;     /* [T, N, dof]  desired velocities                                */
-  double* step_actions;  /* [T, N, dof]  clipped controller actions                        */
-  float* step_obs;       /* [T, N, obs_dim + time_aware]  full (unmasked) observations     */
+  float* positions;      /* [T, dof, N]  desired positions                                 */
+  float* velocities;     /* [T, dof, N]  desired velocities                                */
+  double* step_actions;  /* [T, dof, N]  clipped controller actions                        */
+  float* step_obs;       /* [T, obs_dim + time_aware, N]  full (unmasked) observations     */
   double* step_rewards;  /* [T, N]                                                         */
   uint8_t* is_collided;  /* [T, N]  HoleReacher / ViaPointReacher info                     */
   uint8_t* is_success;   /* [T, N]  HoleReacher / ViaPointReacher info                     */
-  double* end_effector;  /* [T, N, 2] HoleReacher / ViaPointReacher info                   */
+  double* end_effector;  /* [T, 2, N] HoleReacher / ViaPointReacher info                   */
   double* reward_dist;   /* [T, N]  SimpleReacher info                                     */
   double* reward_ctrl;   /* [T, N]  SimpleReacher info                                     */
   int64_t* inner_steps;  /* [FGX_INNER_STEPS_LEN] zero-initialised partial counters: their sum  */
