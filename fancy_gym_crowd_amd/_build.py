@@ -59,8 +59,11 @@ def _hipcc():
 
 
 # per-unit extra flags: k_episode_jl's one-joint lanes gain nothing from SLP-pairing consecutive
-# samples (the table entries of two rows need SGPR shuffles first): plain f32 fmas
-UNIT_FLAGS = {"fgx_ep_jl.hip": ["-fno-slp-vectorize"]}
+# samples (the table entries of two rows need SGPR shuffles first): plain f32 fmas.  Its epilogue
+# calls ocml's sincos (FGX_OCML_SINCOS, csrc/fgx_trig.h; bit-identical to the inlined restatement):
+# 1-2% faster for jl (profiles/r03_ab_s4.jsonl), where the inlined form's registers cost more than
+# the large-argument path it skips.  Device code is not linked across units, so each unit keeps its own.
+UNIT_FLAGS = {"fgx_ep_jl.hip": ["-fno-slp-vectorize", "-DFGX_OCML_SINCOS"]}
 
 
 def _deps(path, seen=None):

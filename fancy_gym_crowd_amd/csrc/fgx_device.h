@@ -165,6 +165,15 @@ __device__ __forceinline__ int wave_max(int x) {
   for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
   return __builtin_amdgcn_readfirstlane(x);
 }
+// min of x in [0, 65535] over the ACTIVE lanes (divergent code allowed): 16 ballots fix the bits from
+// the top, m keeps the minimum's bits above b; wave-uniform result
+__device__ __forceinline__ int wave_min_active(int x) {
+  int m = 0;
+#pragma unroll
+  for (int b = 15; b >= 0; --b)
+    if (__ballot(((x ^ m) >> b) == 0) == 0) m |= 1 << b;
+  return m;
+}
 
 // ------------------------------------------------------------------ exact small helpers
 __device__ __forceinline__ double np_max(double x, double lo) { return (x != x) ? x : (x > lo ? x : lo); }

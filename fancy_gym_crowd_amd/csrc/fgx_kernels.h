@@ -800,12 +800,15 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   // sample (collision) and keep their step rewards in s.rew for lengths above 128.
   const int Te = (MP == MP_GIVEN && s.plan_len) ? s.plan_len[e] : c.T;
   // the per-step info rows L..T-1: the full desired plan (black_box_wrapper.py:245-246), NaN (0 for
-  // the flags) in the per-step arrays after trajectory_length; gen: the plan's generator at sample L
+  // the flags) in the per-step arrays after trajectory_length; gen: the plan's generator at sample L.
+  // The wave walks the rows together from its smallest L (lanes idle below their own), so every
+  // store instruction covers one row of the [T, X, N] arrays: consecutive envs, not X lines per lane.
   auto pad_info = [&](int L, auto& gen) {
     const double dnan = __builtin_nan("");
     const float fnan = __builtin_nanf("");
     float pp[NL], pv[NL];
-    for (int kk = L; kk < c.T; ++kk) {
+    for (int kk = wave_min_active(min(L, c.T)); kk < c.T; ++kk) {
+      if (kk < L) continue;
       const int64_t ek = (int64_t)kk * N + e;        // [T, N] arrays
       const int64_t ed = (int64_t)kk * NL * N + e;   // [T, dof, N] arrays: component d at ed + d N
       if (o.positions && MP != MP_GIVEN) {

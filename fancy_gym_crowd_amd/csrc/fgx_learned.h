@@ -75,10 +75,11 @@ __global__ __launch_bounds__(256) void k_traj_env(DevCfg c, DevState s, const fl
       }
     }
   }
-  if (info_pos)   // the plan ends at T_e: NaN beyond (info arrays are [T, dof, N])
-    for (int k = Te; k < c.T; ++k)
+  if (info_pos)   // the plan ends at T_e: NaN beyond (info arrays are [T, dof, N]; rows walked by the wave)
+    for (int k = wave_min_active(min(Te, c.T)); k < c.T; ++k)
 #pragma unroll
       for (int d = 0; d < NL; ++d) {
+        if (k < Te) continue;
         info_pos[((int64_t)k * NL + d) * N + e] = __builtin_nanf("");
         info_vel[((int64_t)k * NL + d) * N + e] = __builtin_nanf("");
       }

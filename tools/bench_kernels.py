@@ -128,22 +128,30 @@ if __name__ == "__main__":
                 env_kwargs={"allow_wall_collision": True})
         episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_self_collision", reps=5,
                 env_kwargs={"allow_self_collision": True})
-    if "log" in which:   # info_level=2 (verbose 2 per-step arrays) through the public step()
-        for env_id in ("fancy_ProMP/LongSimpleReacher-v0", "fancy_ProDMP/HoleReacher-v0"):
+    log_ids = [e for w, e in (("log", None), ("logsimple", "fancy_ProMP/LongSimpleReacher-v0"),
+                              ("loghole", "fancy_ProDMP/HoleReacher-v0")) if w in which]
+    if log_ids:   # info_level=2 (verbose 2 per-step arrays) through the public step(); logsimple /
+        # loghole: one env id only (PMC passes keep one kernel)
+        ids = ("fancy_ProMP/LongSimpleReacher-v0", "fancy_ProDMP/HoleReacher-v0") if None in log_ids else log_ids
+        for env_id in ids:
             env = fgx.make(env_id, num_envs=65536, device=dev, info_level=2)
             env.reset(seed=0)
             params = torch.randn((65536, env.n_params), device=dev)
             for _ in range(2):
-                env.step(params)
+                info = env.step(params)[4]
             torch.cuda.synchronize()
+            # bytes the kernel writes per step into the per-step info arrays (their full [T, X, N] extents)
+            ib = sum(v.untyped_storage().nbytes() for k, v in info.items() if isinstance(v, torch.Tensor)
+                     and v.dim() >= 2 and v.shape[1] == env.T)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(5):
                 env.step(params)
             e1.record()
             torch.cuda.synchronize()
-            print(json.dumps(dict(kernel="step(info_level=2)", config=env_id, envs=65536,
-                                  us_per_step=e0.elapsed_time(e1) / 5 * 1e3)), flush=True)
+            us = e0.elapsed_time(e1) / 5 * 1e3
+            print(json.dumps(dict(kernel="step(info_level=2)", config=env_id, envs=65536, us_per_step=us,
+                                  info_bytes=ib, info_GBps_step_wall=ib / us / 1e3)), flush=True)
             del env
             torch.cuda.empty_cache()
     if "scan" in which:   # metric env over the envs-per-GPU axis (occupancy / tail effects)

@@ -11,7 +11,11 @@ the metric's) and the sub-directories written by tools/gpu_pmc_r03.sh, one rocpr
   busy/   --pmc VALUBusy
   mix/    --pmc SQ_INSTS_VALU SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64
   mfma/   --pmc SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES   (k_traj_mfma)
-Case directory names are n<ENVS> or n<ENVS>_<tag>.
+  stall/  --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
+          SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_WR
+Case directory names are n<ENVS> or n<ENVS>_<tag>; a tag ending in "log" is the info_level=2 step
+(`tools/bench_kernels.py log{simple,hole}`): its entry's kernel is "<family>+info_level2" (bench.py
+never matches it) and carries the info-array bytes the bench_kernels line reports.
 
 Per counter the value of one dispatch is the sum over its rows (instances / XCDs); the entry keeps
 the median over the dispatches of the profiled kernel.  HBM traffic follows MI355X_MICROARCH.md's
@@ -31,7 +35,7 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD = "fancy_ProMP/LongSimpleReacher-v0"
 T = 200
-PARTS = ("fetch", "write", "issue", "busy", "mix", "mfma")
+PARTS = ("fetch", "write", "issue", "busy", "mix", "mfma", "stall")
 
 
 def kernel_family(name):
@@ -102,6 +106,16 @@ def entry(d, envs, workload, bid, rnd, want=None):
         e["valu_mix_source"] = "PMC SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 + SQ_INSTS_VALU_CVT"
     if "VALUBusy" in counters:
         e["valu_busy_pct"] = counters["VALUBusy"]
+    if "SQ_WAVE_CYCLES" in counters and counters["SQ_WAVE_CYCLES"]:
+        wc = counters["SQ_WAVE_CYCLES"]
+        e["stall"] = {"wait_any_frac": counters.get("SQ_WAIT_ANY", 0.0) / wc,
+                      "wait_inst_any_frac": counters.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                      "valu_active_frac": counters.get("SQ_ACTIVE_INST_VALU", 0.0) / wc,
+                      # mean active lanes per VALU instruction cycle (64 = no idle lanes)
+                      "valu_lanes_per_active_cycle": (counters.get("SQ_THREAD_CYCLES_VALU", 0.0) /
+                                                      counters["SQ_ACTIVE_INST_VALU"])
+                      if counters.get("SQ_ACTIVE_INST_VALU") else None,
+                      "vmem_wr_instr": counters.get("SQ_INSTS_VMEM_WR")}
     if "SQ_INSTS_VALU_MFMA_MOPS_F32" in counters:
         e["mfma_f32_instr"] = counters.get("SQ_INSTS_VALU_MFMA_F32")
         e["mfma_f32_flops"] = counters["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
@@ -128,6 +142,16 @@ def main():
                 entries.append(e)
         e = entry(d, envs, workload, bid, a.round)
         if e is not None and e["kernel"] != "k_traj_mfma":
+            if os.path.basename(d).endswith("log"):
+                e["kernel"] += "+info_level2"
+                e["info_level"] = 2
+                for part in ("fetch", "write", "stall"):   # the bench_kernels line of the pass
+                    lp = os.path.join(d, part + ".log")
+                    for ln in (open(lp) if os.path.exists(lp) else []):
+                        if ln.startswith("{") and "info_bytes" in ln:
+                            e["bench_kernels_" + part] = json.loads(ln)
+                if "traffic_bytes_per_launch" in e and "bench_kernels_write" in e:
+                    e["info_bytes_per_launch"] = e["bench_kernels_write"]["info_bytes"]
             entries.append(e)
     out = {"method": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc_r03.sh); median over "
                      "dispatches of the per-dispatch sum over instances; traffic = (2*FETCH_SIZE + "
