@@ -154,6 +154,17 @@ __device__ __forceinline__ void count_inner(long long* base, long long sum, bool
     atomicAdd((unsigned long long*)(base + (size_t)(w % kInnerSlots) * kInnerStride), (unsigned long long)sum);
 }
 
+// Stores into the per-step info arrays (write-once streams of up to GBs per BB step).  FGX_INFO_NT
+// (A/B build): non-temporal stores.
+template <typename T>
+__device__ __forceinline__ void info_st(T* p, T x) {
+#ifdef FGX_INFO_NT
+  __builtin_nontemporal_store(x, p);
+#else
+  *p = x;
+#endif
+}
+
 // ------------------------------------------------------------------ wave reductions (all 64 lanes active)
 __device__ __forceinline__ int wave_min(int x) {
 #pragma unroll
@@ -383,7 +394,7 @@ struct Env {
     }
   }
 
-  // reset draws (simple_reacher.py:46-54,85-96; hole_reacher.py:242-294; base_reacher.py:73-93)
+  // reset draws (simple_reacher.py:46-54,85-96; hole_reacher.py:60-112; base_reacher.py:73-93)
   // rs: random_start of this reset (the constructor's, or reset(options={'random_start': ...}),
   // base_reacher.py:77-80)
   __device__ __forceinline__ void first_joint(Pcg64& r, bool rs) {

@@ -18,7 +18,7 @@
 namespace fgx {
 
 // ============================================================================ obs
-// Env observation (simple_reacher.py:75-83 / hole_reacher.py:296-306) [+ t/max_steps,
+// Env observation (simple_reacher.py:75-83 / hole_reacher.py:114-124) [+ t/max_steps,
 // utils/wrappers.py:58-59], context-masked when `ctx` (black_box_wrapper.py:90-95), written
 // straight to up to two destinations (no private arrays: nothing spills to scratch).
 // fresh: v was just reset (Env::reset): q = [q0, +0, ..., +0] and fk() has run, so cos / sin of
@@ -33,7 +33,7 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
-    if (d1) d1[p * s1] = x;
+    if (d1) { if (s1 != 1) info_st(d1 + p * s1, x); else d1[p] = x; }
     if (d2) d2[p] = x;
     ++p;
   };
@@ -426,7 +426,7 @@ struct Traj {
 // ============================================================================ env substep
 // One env.step with the (clipped) action a (f64) / a32 (when the action array is float32).
 // base_reacher_torque.py:20-37, base_reacher_direct.py:20-38, simple_reacher.py:56-70,
-// hole_reacher.py:255-259, hr_simple_reward.py:19-53, hr_dist_vel_acc_reward.py:20-60,
+// hole_reacher.py:73-77, hr_simple_reward.py:19-53, hr_dist_vel_acc_reward.py:20-60,
 // hr_unbounded_reward.py:17-59, viapoint_reacher.py:79-111.  Returns the reward; FK is
 // refreshed for the direct envs always and for SimpleReacher only when the reward needs it or
 // `fk_always`.
@@ -803,27 +803,30 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   // the flags) in the per-step arrays after trajectory_length; gen: the plan's generator at sample L.
   // The wave walks the rows together from its smallest L (lanes idle below their own), so every
   // store instruction covers one row of the [T, X, N] arrays: consecutive envs, not X lines per lane.
-  auto pad_info = [&](int L, auto& gen) {
+  auto pad_row = [&](int kk, auto& gen) {
     const double dnan = __builtin_nan("");
     const float fnan = __builtin_nanf("");
     float pp[NL], pv[NL];
-    for (int kk = wave_min_active(min(L, c.T)); kk < c.T; ++kk) {
-      if (kk < L) continue;
+    {
       const int64_t ek = (int64_t)kk * N + e;        // [T, N] arrays
       const int64_t ed = (int64_t)kk * NL * N + e;   // [T, dof, N] arrays: component d at ed + d N
       if (o.positions && MP != MP_GIVEN) {
         gen.at(c, kk, pp, pv);
-        for (int d = 0; d < NL; ++d) { o.positions[ed + d * N] = pp[d]; o.velocities[ed + d * N] = pv[d]; }
+        for (int d = 0; d < NL; ++d) { info_st(o.positions + ed + d * N, pp[d]); info_st(o.velocities + ed + d * N, pv[d]); }
       }
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) o.step_actions[ed + d * N] = dnan;
-      if (o.step_rewards) o.step_rewards[ek] = dnan;
+        for (int d = 0; d < NL; ++d) info_st(o.step_actions + ed + d * N, dnan);
+      if (o.step_rewards) info_st(o.step_rewards + ek, dnan);
       if (o.step_obs)
-        for (int q = 0; q < c.full_dim; ++q) o.step_obs[((int64_t)kk * c.full_dim + q) * N + e] = fnan;
-      if (o.is_collided) { o.is_collided[ek] = 0; o.is_success[ek] = 0; }
-      if (o.end_effector) { o.end_effector[2 * kk * N + e] = dnan; o.end_effector[(2 * kk + 1) * N + e] = dnan; }
-      if (o.reward_dist) { o.reward_dist[ek] = dnan; o.reward_ctrl[ek] = dnan; }
+        for (int q = 0; q < c.full_dim; ++q) info_st(o.step_obs + ((int64_t)kk * c.full_dim + q) * N + e, fnan);
+      if (o.is_collided) { info_st(o.is_collided + ek, (uint8_t)0); info_st(o.is_success + ek, (uint8_t)0); }
+      if (o.end_effector) { info_st(o.end_effector + 2 * kk * N + e, dnan); info_st(o.end_effector + (2 * kk + 1) * N + e, dnan); }
+      if (o.reward_dist) { info_st(o.reward_dist + ek, dnan); info_st(o.reward_ctrl + ek, dnan); }
     }
+  };
+  auto pad_info = [&](int L, auto& gen) {
+    for (int kk = wave_min_active(min(L, c.T)); kk < c.T; ++kk)
+      if (kk >= L) pad_row(kk, gen);
   };
   if constexpr (LOG) {   // trajectory validity (the logging instantiation serves valid_flags != 0)
     if (c.valid_flags &&
@@ -925,19 +928,19 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
       const int64_t ek = (int64_t)k * N + e;
       const int64_t ed = (int64_t)k * NL * N + e;
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) o.step_actions[ed + d * N] = a[d];
+        for (int d = 0; d < NL; ++d) info_st(o.step_actions + ed + d * N, a[d]);
       if (o.positions && MP != MP_GIVEN)
-        for (int d = 0; d < NL; ++d) { o.positions[ed + d * N] = pos[d]; o.velocities[ed + d * N] = vel[d]; }
-      if (o.step_rewards) o.step_rewards[ek] = r.reward;
+        for (int d = 0; d < NL; ++d) { info_st(o.positions + ed + d * N, pos[d]); info_st(o.velocities + ed + d * N, vel[d]); }
+      if (o.step_rewards) info_st(o.step_rewards + ek, r.reward);
       // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
       if (o.step_obs) emit_obs(c, v, false, o.step_obs + (int64_t)k * c.full_dim * N + e, nullptr, false, true,
                                nullptr, nullptr, N);
       if (ENV != ENV_SIMPLE) {
-        if (o.is_collided) { o.is_collided[ek] = r.coll; o.is_success[ek] = r.success; }
-        if (o.end_effector) { o.end_effector[2 * k * N + e] = v.jx[NL]; o.end_effector[(2 * k + 1) * N + e] = v.jy[NL]; }
+        if (o.is_collided) { info_st(o.is_collided + ek, (uint8_t)r.coll); info_st(o.is_success + ek, (uint8_t)r.success); }
+        if (o.end_effector) { info_st(o.end_effector + 2 * k * N + e, v.jx[NL]); info_st(o.end_effector + (2 * k + 1) * N + e, v.jy[NL]); }
       } else if (o.reward_dist) {
-        o.reward_dist[ek] = r.rdist;
-        o.reward_ctrl[ek] = r.rctrl;
+        info_st(o.reward_dist + ek, r.rdist);
+        info_st(o.reward_ctrl + ek, r.rctrl);
       }
     }
     bool replan_now = (k == k_replan);
@@ -1178,13 +1181,31 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
 #undef FGX_SAMPLE
   }
   FGX_STAMP(o, e, 2);
-  while (!stop && k < Te) {
-    stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, LOG || c.sched_state);
-    ++k;
+  int L = 0x7fffffff;   // samples executed (trajectory_length)
+  if constexpr (LOG) {
+    // the wave walks the plan rows together (k is wave-uniform here: no fast blocks with LOG): a
+    // lane whose env has stopped pads its row k beside the samples of the lanes still running, so
+    // every info store covers the wave's consecutive envs in one row, then rows k..T-1 of all lanes
+    for (;; ++k) {
+      const bool act = !stop && k < Te;
+      if (__ballot(act) == 0) break;
+      if (act) {
+        stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, true);
+      } else {
+        L = min(L, k);
+        if (k < c.T) pad_row(k, tg);
+      }
+    }
+    L = min(L, k);
+    pad_info(k, tg);
+  } else {
+    while (!stop && k < Te) {
+      stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, c.sched_state);
+      ++k;
+    }
+    L = k;
   }
   FGX_STAMP(o, e, 3);
-  const int L = k;   // samples executed (trajectory_length)
-  if (LOG) pad_info(L, tg);
   // the epilogue needs FK of the final q; a last sample at env step >= 199 (always a generic one)
   // has just computed it for its reward
   if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();

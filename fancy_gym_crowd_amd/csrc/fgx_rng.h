@@ -3,7 +3,7 @@
 // The reference seeds each env with gymnasium seeding.np_random(seed) =
 // np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed))) [EXT-H] and draws with
 // Generator.uniform / Generator.choice (base_reacher.py:82, simple_reacher.py:87-92,
-// hole_reacher.py:261-275).  This header restates those numpy algorithms bit-exactly:
+// hole_reacher.py:79-112).  This header restates those numpy algorithms bit-exactly:
 //   SeedSequence(seed).generate_state(4, uint64)   (numpy/random/bit_generator.pyx)
 //   PCG64 XSL-RR 128/64, set_seed, next64, buffered next32 (numpy/random/src/pcg64)
 //   next_double = (next64 >> 11) * 2^-53; uniform(lo, hi) = lo + (hi - lo) * next_double

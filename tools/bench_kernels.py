@@ -83,6 +83,45 @@ def trajectory(env_id, N, force_valu=False):
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
 
+def mfma_ab(env_id="fancy_ProMP/LongSimpleReacher-v0", N=65536, reps=20):
+    """The MP contraction on the matrix cores vs fused on the VALU: (a) fgx_step = k_episode, the
+    contraction as f32 fma chains inside the episode loop; (b) fgx_trajectory (k_traj_mfma: the
+    basis GEMM on v_mfma_f32_32x32x2_f32, plans [N, T, dof] to HBM) + fgx_step_traj
+    (k_episode<MP_GIVEN>: the same episode reading the plans).  Same returns bit for bit."""
+    import ctypes
+    res = {}
+    for mode in ("fused_valu", "mfma_plans"):
+        env = fgx.make(env_id, num_envs=N, device=dev, info_level=0)
+        env.reset(seed=0)
+        T, n = env.T, env.dof
+        params = torch.from_numpy(np.random.default_rng(1234).standard_normal((N, env.n_params), dtype=np.float32)).to(dev)
+        obs = torch.empty((N, env.out_dim), device=dev)
+        ret = torch.empty(N, dtype=torch.float64, device=dev)
+        te = torch.empty(N, dtype=torch.uint8, device=dev)
+        tr = torch.empty(N, dtype=torch.uint8, device=dev)
+        tl = torch.empty(N, dtype=torch.int32, device=dev)
+        pos = torch.empty((N, T, n), device=dev)
+        vel = torch.empty_like(pos)
+        lib, h = env._eng.lib, env._eng.h
+        p = [ctypes.c_void_p(x.data_ptr()) for x in (params, pos, vel, obs, ret, te, tr, tl)]
+        if mode == "fused_valu":
+            fn = lambda: lib.fgx_step(h, p[0], p[3], p[4], p[5], p[6], p[7], None, None, 1, env._eng.stream())  # noqa: E731
+        else:
+            def fn():
+                lib.fgx_trajectory(h, p[0], p[1], p[2], env._eng.stream())
+                lib.fgx_step_traj(h, p[1], p[2], p[3], p[4], p[5], p[6], p[7], None, None, 1, env._eng.stream())
+        t = timed(fn, reps=reps)
+        env.reset(seed=0)
+        fn()
+        torch.cuda.synchronize()
+        res[mode] = ret.cpu().numpy().copy()
+        print(json.dumps(dict(kernel=mode, config=env_id, envs=N, us_per_bb_step=t * 1e6,
+                              inner_steps_per_s=float(tl.sum().item()) / t)), flush=True)
+        del env
+    print(json.dumps(dict(kernel="mfma_ab", returns_bit_equal=bool(np.array_equal(
+        res["fused_valu"].view(np.int64), res["mfma_plans"].view(np.int64))))), flush=True)
+
+
 def step_raw(env_id, N, final_obs=True):
     """k_step_raw through fgx_step_raw as StepVectorEnv.step calls it (with final_obs)."""
     env = fgx.make(env_id, num_envs=N, device=dev, info_level=0)
@@ -206,5 +245,8 @@ if __name__ == "__main__":
                        "fancy/ViaPointReacher-v0"):
             step_raw(env_id, 1 << 20)
         step_raw("fancy/SimpleReacher-v0", 1 << 20, final_obs=False)
+    if "mfmaab" in which:
+        mfma_ab()
+        mfma_ab("fancy_ProDMP/LongSimpleReacher-v0")
     if "raw1" in which:   # config 1 alone (PMC passes)
         step_raw("fancy/SimpleReacher-v0", 1 << 20)

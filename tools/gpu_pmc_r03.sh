@@ -7,7 +7,7 @@
 # Counter groups stay within one block's limits (<= 8 SQ, FETCH_SIZE 3 TCC, WRITE_SIZE 2 TCC).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_r03
+OUT=${OUT:-gpurun_out/pmc_r03}
 mkdir -p $OUT
 METRIC=fancy_ProMP/LongSimpleReacher-v0
 # a tag ending in _log runs the info_level=2 step (tools/bench_kernels.py log{simple,hole}) instead

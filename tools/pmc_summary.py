@@ -127,6 +127,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("--round", default="r03")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
+                    help="summary path (the default is what bench.py reads)")
+    ap.add_argument("--no-copy", action="store_true", help="do not copy the counter CSVs into profiles/")
     ap.add_argument("--build-id", default=None, help="build id of the profiled library (default: the "
                     "hash of the sources in this tree)")
     a = ap.parse_args()
@@ -158,7 +161,7 @@ def main():
                      "WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count); valu_mix from the mix pass",
            "entries": entries}
     # the counter CSVs the entries come from travel with the summary
-    for d in sorted(glob.glob(os.path.join(a.src, "n*"))):
+    for d in ([] if a.no_copy else sorted(glob.glob(os.path.join(a.src, "n*")))):
         dd0 = os.path.join(ROOT, "profiles", f"{a.round}_pmc", os.path.basename(d))
         for path in glob.glob(os.path.join(d, "*", "**", "*_counter_collection.csv"), recursive=True):
             part = os.path.relpath(path, d).split(os.sep)[0]
@@ -167,8 +170,7 @@ def main():
         if os.path.exists(os.path.join(d, "workload.txt")):
             os.makedirs(dd0, exist_ok=True)
             shutil.copy(os.path.join(d, "workload.txt"), os.path.join(dd0, "workload.txt"))
-    dst = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    with open(dst, "w") as f:
+    with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
