@@ -83,7 +83,8 @@ EXPORTS = {
     "fgx_episode_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "fgx_selftest_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
-EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2"}
+EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2",
+                   5: "k_episode_pair"}
 
 _LIB = None
 

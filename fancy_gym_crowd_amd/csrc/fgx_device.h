@@ -176,6 +176,15 @@ __device__ __forceinline__ int wave_max(int x) {
   for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
   return __builtin_amdgcn_readfirstlane(x);
 }
+// the partner lane's value in lane pairs (2i, 2i + 1): DPP quad_perm [1, 0, 3, 2]; both lanes of a
+// pair are always active together (k_episode_pair)
+__device__ __forceinline__ int pair_swap32(int x) { return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ double pair_swap(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)pair_swap32((int)(unsigned)b), hi = (unsigned)pair_swap32((int)(unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ bool pair_or(bool x) { return ((int)x | pair_swap32((int)x)) != 0; }
 // min of x in [0, 65535] over the ACTIVE lanes (divergent code allowed): 16 ballots fix the bits from
 // the top, m keeps the minimum's bits above b; wave-uniform result
 __device__ __forceinline__ int wave_min_active(int x) {
@@ -551,7 +560,14 @@ struct Env {
     for (int k = 0; k < NL; ++k) {
       const double y0 = jy[k], y1 = jy[k + 1];
       if (y0 >= 0.0 && y1 >= 0.0 && nd <= 0.0) continue;
-      const double bx = jx[k], by = jy[k], ck = c[k], sk = s[k];
+      hit |= link_wall(left, right, nd, jx[k], jy[k], c[k], s[k]);
+    }
+    return hit;
+  }
+  // the wall test of one submerged link starting at (bx, by) with direction (ck, sk)
+  static __device__ __forceinline__ bool link_wall(double left, double right, double nd, double bx, double by,
+                                                   double ck, double sk) {
+    {
       // lin_j = np.linspace(0, 1, 100)[j] = j * RN(1/99), last = 1 (computed, not loaded: the
       // binary searches would otherwise chain dependent memory loads)
       auto lin = [](int j) { return j == 99 ? 1.0 : (double)j * (1.0 / 99.0); };
@@ -599,9 +615,88 @@ struct Env {
       const bool c1 = max(xl0, yg0) < min(xl1, yg1);
       const bool c2 = max(xr0, yg0) < min(xr1, yg1);
       const bool c3 = max(max(xL0, xR0), yd0) < min(min(xL1, xR1), yd1);
-      hit |= c1 || c2 || c3;
+      return c1 || c2 || c3;
     }
-    return hit;
+  }
+
+  // ---------------------------------------------------------------- lane pairs (k_episode_pair)
+  // Both lanes of a pair (2i, 2i + 1) hold the same env and run the same step; p = this lane's
+  // parity.  The costly parts of a HoleReacher step are divided between them: lane p evaluates the
+  // sincos of the cumulative angles p, p + 2, ..., every other segment pair of the self-collision
+  // test and every other link of the wall test, and takes the partner's results over a DPP lane
+  // swap.  Each lane ends with exactly the values fk() / self_collision() / wall_collision()
+  // compute: the same expressions on the same operands, only evaluated in the other lane.  The
+  // selections below use the lane parity as data (v_cndmask), never as a branch, so both lanes'
+  // shares issue as one instruction stream.
+  __device__ __forceinline__ void fk_pair(int p) {
+    constexpr int H = (NL + 1) / 2;
+    double ang[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) ang[k] = (k == 0) ? q[0] : ang[k - 1] + q[k];
+    double ms[H], mc[H], os[H], oc[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const double a = p ? ang[min(2 * h + 1, NL - 1)] : ang[2 * h];
+      fgx_sincos(a, &ms[h], &mc[h]);
+      os[h] = pair_swap(ms[h]);
+      oc[h] = pair_swap(mc[h]);
+    }
+    double x = 0.0, y = 0.0;
+    jx[0] = 0.0; jy[0] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int h = k >> 1;
+      // angle k is lane (k & 1)'s (both lanes evaluate the last one when NL is odd)
+      const bool own = (2 * h + 1 >= NL) || ((k & 1) == p);
+      const double cs = own ? mc[h] : oc[h], sn = own ? ms[h] : os[h];
+      c[k] = cs; s[k] = sn;
+      x = (k == 0) ? cs : x + cs;
+      y = (k == 0) ? sn : y + sn;
+      jx[k + 1] = 0.0 + x;
+      jy[k + 1] = 0.0 + y;
+    }
+  }
+  // segment pair n of the self-collision test in index order: (i, j), j >= i + 2
+  static constexpr int seg_pair(int n, int which) {
+    int m = 0;
+    for (int i = 0; i < NL; ++i)
+      for (int j = i + 2; j < NL; ++j) {
+        if (m == n) return which ? j : i;
+        ++m;
+      }
+    return 0;
+  }
+  __device__ __forceinline__ bool self_collision_pair(int p) const {
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      if (q[k] > M_PI || q[k] < -M_PI) return true;   // base_reacher.py:38-39,111
+    constexpr int NP = (NL - 1) * (NL - 2) / 2;
+    bool hit = false;
+#pragma unroll
+    for (int t = 0; 2 * t < NP; ++t) {   // lane p: pair 2t + p (lane 1 repeats pair 2t past the end)
+      const int n0 = 2 * t, n1 = (2 * t + 1 < NP) ? 2 * t + 1 : 2 * t;
+      const int i0 = seg_pair(n0, 0), j0 = seg_pair(n0, 1), i1 = seg_pair(n1, 0), j1 = seg_pair(n1, 1);
+      const double ax = p ? jx[i1] : jx[i0], ay = p ? jy[i1] : jy[i0];
+      const double bx = p ? jx[i1 + 1] : jx[i0 + 1], by = p ? jy[i1 + 1] : jy[i0 + 1];
+      const double cx = p ? jx[j1] : jx[j0], cy = p ? jy[j1] : jy[j0];
+      const double dx = p ? jx[j1 + 1] : jx[j0 + 1], dy = p ? jy[j1 + 1] : jy[j0 + 1];
+      hit |= (ccw(ax, ay, cx, cy, dx, dy) != ccw(bx, by, cx, cy, dx, dy)) &&
+             (ccw(ax, ay, bx, by, cx, cy) != ccw(ax, ay, bx, by, dx, dy));
+    }
+    return pair_or(hit);
+  }
+  __device__ __forceinline__ bool wall_collision_pair(const DevCfg& cf, int p) const {
+    const double left = hx - hw / 2, right = hx + hw / 2, nd = -hd;
+    bool hit = false;
+#pragma unroll
+    for (int t = 0; 2 * t < NL; ++t) {   // lane p: link 2t + p (none for lane 1 past the end)
+      const int k0 = 2 * t, k1 = (2 * t + 1 < NL) ? 2 * t + 1 : 2 * t;
+      const bool none = (2 * t + 1 >= NL) && p;
+      const double y0 = p ? jy[k1] : jy[k0], y1 = p ? jy[k1 + 1] : jy[k0 + 1];
+      if (none || (y0 >= 0.0 && y1 >= 0.0 && nd <= 0.0)) continue;
+      hit |= link_wall(left, right, nd, p ? jx[k1] : jx[k0], y0, p ? c[k1] : c[k0], p ? s[k1] : s[k0]);
+    }
+    return pair_or(hit);
   }
 };
 

@@ -43,7 +43,7 @@ namespace fgx {
 //    its exchange rows stopped conflicting on LDS banks).
 // k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
 // wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4 };
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_PAIR = 5 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -59,7 +59,14 @@ inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave
 // k_episode or k_episode_w2: 5-link SimpleReacher without per-step info past one k_episode round
 // (two resident waves per SIMD, profiles/r02_w2_ab.jsonl); FGX_EPISODE_KERNEL=classic keeps k_episode
 inline bool w2_applies(const DevCfg& c, bool log) { return c.env == ENV_SIMPLE && c.nl == 5 && !log; }
+// k_episode_pair: 5-link HoleReacher without per-step info (two lanes per env, fgx_kernels.h);
+// FGX_EPISODE_KERNEL=classic keeps k_episode
+inline bool pair_applies(const DevCfg& c, bool log) { return c.env == ENV_HOLE && c.nl == 5 && !log; }
 inline int classic_choice(const DevCfg& c, bool log) {
+  if (pair_applies(c, log)) {
+    const char* v = std::getenv("FGX_EPISODE_KERNEL");
+    return (v && std::strcmp(v, "classic") == 0) ? EK_CLASSIC : EK_PAIR;
+  }
   if (!w2_applies(c, log)) return EK_CLASSIC;
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
     if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
@@ -149,6 +156,16 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
+  }
+  if constexpr (ENV == ENV_HOLE && NL == 5) {
+    if (classic_choice(c, log) == EK_PAIR) {
+      const int pblocks = (int)((2 * c.N + threads - 1) / threads);
+      hipLaunchKernelGGL((k_episode_pair<ENV, MP, CTRL, NL, NB>), dim3(pblocks), dim3(threads), lds, stream, c, s,
+                         params, dpos, dvel, o);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) { err = std::string("k_episode_pair launch: ") + hipGetErrorString(e); return -2; }
+      return 0;
+    }
   }
   if constexpr (ENV == ENV_SIMPLE && NL == 5) {
     if (classic_choice(c, log) == EK_CLASSIC_W2 &&

@@ -435,9 +435,12 @@ struct StepOut {
   bool coll, success;
 };
 
-template <int ENV, bool F32, int NL, bool MAYFK = true>
+// PAIR: k_episode_pair's lane pairs share the FK sincos and the collision tests (pp = lane parity)
+template <int ENV, bool F32, int NL, bool MAYFK = true, bool PAIR = false>
 __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const double* a, const float* a32,
-                                           bool fk_always) {
+                                           bool fk_always, int pp = 0) {
+  auto self_c = [&]() { if constexpr (PAIR) return v.self_collision_pair(pp); else return v.self_collision(); };
+  auto wall_c = [&]() { if constexpr (PAIR) return v.wall_collision_pair(c, pp); else return v.wall_collision(c); };
   StepOut r;
   r.coll = false;
   r.success = false;
@@ -492,7 +495,8 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       v.q[d] = v.q[d] + inc;
     }
     if (F32) v.flags |= 1u;
-    v.fk();
+    if constexpr (PAIR) v.fk_pair(pp);
+    else v.fk();
     // sum(action**2) == sum(qd**2) after the step (f32 for a float32 action array)
     double act_sq;
     if (F32) {
@@ -506,7 +510,7 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       for (int d = 1; d < NL; ++d) act_sq = act_sq + a[d] * a[d];
     }
     if (ENV == ENV_VIA) {   // viapoint_reacher.py:79-111
-      r.coll = c.allow_self ? false : v.self_collision();
+      r.coll = c.allow_self ? false : self_c();
       // 5e-8 * np.sum(action**2): a float32 sum stays float32 (NEP 50)
       const double pen_ctrl = F32 ? (double)(5e-8f * (float)act_sq) : 5e-8 * act_sq;
       if (r.coll) {
@@ -519,8 +523,8 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       }
     } else if (c.rew_fct == REW_VEL_ACC) {   // hr_dist_vel_acc_reward.py:20-60
       if (!(v.flags & 4u)) {
-        const bool sc = c.allow_self ? false : v.self_collision();
-        const bool wc = c.allow_wall ? false : v.wall_collision(c);
+        const bool sc = c.allow_self ? false : self_c();
+        const bool wc = c.allow_wall ? false : wall_c();
         if (sc || wc) v.flags |= 4u;
         v.cd = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
       }
@@ -539,8 +543,8 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       d = __builtin_fma(coll_cost, -c.penalty, d);
       r.reward = __builtin_fma(0.0, 0.0, d);   // time_cost = 199 - steps is 0 whenever used
     } else if (c.rew_fct == REW_UNBOUNDED) {   // hr_unbounded_reward.py:17-59
-      const bool sc = c.allow_self ? false : v.self_collision();
-      const bool wc = c.allow_wall ? false : v.wall_collision(c);
+      const bool sc = c.allow_self ? false : self_c();
+      const bool wc = c.allow_wall ? false : wall_c();
       r.coll = sc || wc;
       if (st == 180 || r.coll) { v.ex = v.jx[NL]; v.ey = v.jy[NL]; }
       double dr = 0.0;
@@ -552,8 +556,8 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       }
       r.reward = __builtin_fma(acc_cost, -5e-6, dr * 1.0);
     } else {   // hr_simple_reward.py:19-53
-      const bool sc = c.allow_self ? false : v.self_collision();
-      const bool wc = c.allow_wall ? false : v.wall_collision(c);
+      const bool sc = c.allow_self ? false : self_c();
+      const bool wc = c.allow_wall ? false : wall_c();
       r.coll = sc || wc;
       if (st == 199 || r.coll) {
         const double dist = norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
@@ -755,17 +759,23 @@ __device__ inline void invalid_transition(const DevCfg& c, const DevState& s, co
 // ============================================================================ the BB step
 // The body of k_episode (below) and k_episode_w2 (the same code compiled for two resident waves
 // per SIMD).
-template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>
+// PAIR (k_episode_pair): two lanes per env (lanes 2i, 2i + 1 hold env i), both running the whole
+// step; the FK sincos and the collision tests are divided between them (Env::fk_pair).  Every store
+// is made by both lanes with the same value; the inner-step counter takes the even lanes' lengths.
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG, bool PAIR = false>
 __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s, const float* __restrict__ params,
                                              const float* __restrict__ dpos, const float* __restrict__ dvel,
                                              const Outputs& o) {
+  static_assert(!(PAIR && (LOG || ENV == ENV_SIMPLE)), "lane pairs serve the direct envs without per-step info");
   extern __shared__ float lds_tab[];
   if (MP != MP_GIVEN) {
     const int n = c.rows * c.stride;
     for (int i = threadIdx.x; i < n; i += blockDim.x) lds_tab[i] = s.tables[i];
     __syncthreads();
   }
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = PAIR ? (tid >> 1) : tid;
+  const int pp = PAIR ? (int)(threadIdx.x & 1) : 0;
   if (e >= c.N) return;
   const int64_t N = c.N;
   FGX_STAMP(o, e, 6);
@@ -908,7 +918,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
       }
     }
     // ---- env.step
-    const StepOut r = substep<ENV, F32, NL, (J < 0)>(c, v, a, a32, fk_always);
+    const StepOut r = substep<ENV, F32, NL, (J < 0), PAIR>(c, v, a, a32, fk_always, pp);
     if constexpr (J >= 0) {   // fast blocks: no termination, truncation or replanning inside
       // SimpleReacher below env step 199: reward = 0 - ctrl, pushed as acc - ctrl
       if constexpr (ENV != ENV_SIMPLE) ps.template add_fast<J, (PH & 3)>(r.reward);   // (not reached)
@@ -1211,9 +1221,30 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();
   const double ret = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
   FGX_STAMP(o, e, 4);
-  episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc);
+  if constexpr (PAIR) {   // the env's length once: from its even lane
+    if (o.inner_steps) {
+      long long sum = pp ? 0 : L;
+      if (__ballot(1) == ~0ull) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+        count_inner(o.inner_steps, sum, (threadIdx.x & 63) == 0);
+      } else {
+        count_inner(o.inner_steps, sum, true);
+      }
+    }
+  }
+  episode_epilogue(c, s, o, e, v, plans, L, ret, term, trunc, !PAIR);
   FGX_STAMP(o, e, 5);
   FGX_STAMP(o, e, 7);
+}
+
+// HoleReacher with lane pairs (episode_body PAIR): 2N threads, two resident waves per SIMD (<= 256
+// registers), so that 65536 envs fill two waves on each SIMD instead of one
+template <int ENV, int MP, int CTRL, int NL, int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_episode_pair(
+    DevCfg c, DevState s, const float* __restrict__ params, const float* __restrict__ dpos,
+    const float* __restrict__ dvel, Outputs o) {
+  episode_body<ENV, MP, CTRL, NL, NB, false, true>(c, s, params, dpos, dvel, o);
 }
 
 template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>

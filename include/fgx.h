@@ -258,9 +258,10 @@ int fgx_get_tables(void* handle, float* out, void* stream);
 /* The kernel fgx_step launches for this handle with the given info level (>= 2: per-step info
  * arrays): 0 = k_episode (one env per lane), 1 = k_episode_jp (one wave per joint),
  * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs), 3 = k_episode_jl (one lane
- * per env x joint), 4 = k_episode_w2 (k_episode for two resident waves per SIMD); negative on error.
+ * per env x joint), 4 = k_episode_w2 (k_episode for two resident waves per SIMD), 5 = k_episode_pair
+ * (HoleReacher, two lanes per env); negative on error.
  * info_level >= 1 means some per-step output pointer is given (the launch then runs the logging
- * k_episode, as it does for a config with valid_flags).  All five give bit-identical results; the
+ * k_episode, as it does for a config with valid_flags).  All six give bit-identical results; the
  * choice follows measured speed (fgx_dispatch.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 
