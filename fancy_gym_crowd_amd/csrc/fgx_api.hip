@@ -529,6 +529,13 @@ extern "C" int fgx_dbg_stamps(unsigned long long* host, int n) {
 }
 #endif
 
+// per-step info arrays are addressed with 32-bit byte offsets inside one sample's rows (info_st):
+// N < 2^24 keeps kMaxObs rows of f64 below 4 GB (at 65536 envs the arrays are already 2.4 GB)
+static bool info_too_large(const Handle* h, const fgx_info* info) {
+  return info && (info->positions || info->step_actions || info->step_obs || info->step_rewards || info->is_collided ||
+                  info->end_effector || info->reward_dist) && h->dc.N >= (int64_t(1) << 24);
+}
+
 int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t* terminated, uint8_t* truncated,
              int32_t* traj_len, float* final_obs, const fgx_info* info, int32_t autoreset, void* stream) {
   Handle* h = (Handle*)handle;
@@ -541,6 +548,7 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
     return fail(FGX_E_INVALID, "is_collided and is_success must be given together");
   if (info && ((info->reward_dist == nullptr) != (info->reward_ctrl == nullptr)))
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
+  if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
   if (h->learned()) {
     // per-env plans first (and, when requested, the time-major info copies), then the episode
@@ -572,6 +580,7 @@ int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, floa
     return fail(FGX_E_INVALID, "is_collided and is_success must be given together");
   if (info && ((info->reward_dist == nullptr) != (info->reward_ctrl == nullptr)))
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
+  if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
   o.positions = nullptr;
   o.velocities = nullptr;   // the caller already holds the desired trajectories

@@ -155,9 +155,17 @@ __device__ __forceinline__ void count_inner(long long* base, long long sum, bool
 }
 
 // Stores into the per-step info arrays (write-once streams of up to GBs per BB step).  FGX_INFO_NT
-// (A/B build): non-temporal stores.
+// (A/B build): non-temporal stores (round 3: +3% LongSimpleReacher, -11% HoleReacher; not used).
+// row: the array's block of one wave-uniform sample index (k * X * N), idx: the lane's element in it
+// (component * N + env).  The row address is made an SGPR value and the element a 32-bit offset, so
+// the store takes global_store's saddr form: no per-store 64-bit VGPR address arithmetic (fgx_step
+// rejects per-step arrays for N >= 2^24, where 32-bit byte offsets could overflow).
 template <typename T>
-__device__ __forceinline__ void info_st(T* p, T x) {
+__device__ __forceinline__ void info_st(T* row, uint32_t idx, T x) {
+  const uint64_t a = (uint64_t)row;
+  const uint64_t ua = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  T* p = (T*)((char*)ua + (uint64_t)(idx * (uint32_t)sizeof(T)));
 #ifdef FGX_INFO_NT
   __builtin_nontemporal_store(x, p);
 #else
@@ -262,12 +270,26 @@ struct PairwiseSum {
   }
   __device__ __forceinline__ static void push(double* r, double& tail, int pos, double v) {
     const int j = pos & 7;
-    // runtime j: select-chain keeps r[] in registers
+    const int ju = __builtin_amdgcn_readfirstlane(j);
+    if (__ballot(j != ju) == 0) {
+      // the sample index is the same in every active lane (k_episode's generic loop): a scalar
+      // branch picks the slot, no per-lane select chain over the 8 accumulators
+      switch (ju) {
+#define FGX_PUSH_SLOT(Q) case Q: r[Q] = (pos < 8) ? v : r[Q] + v; break;
+        FGX_PUSH_SLOT(0) FGX_PUSH_SLOT(1) FGX_PUSH_SLOT(2) FGX_PUSH_SLOT(3)
+        FGX_PUSH_SLOT(4) FGX_PUSH_SLOT(5) FGX_PUSH_SLOT(6) FGX_PUSH_SLOT(7)
+#undef FGX_PUSH_SLOT
+      }
+      if (ju == 7) tail = comb(r);
+      else tail = tail + v;
+    } else {
+      // runtime j: select-chain keeps r[] in registers
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (q == j) r[q] = (pos < 8) ? v : r[q] + v;
-    if (j == 7) tail = comb(r);
-    else tail = tail + v;
+      for (int q = 0; q < 8; ++q)
+        if (q == j) r[q] = (pos < 8) ? v : r[q] + v;
+      if (j == 7) tail = comb(r);
+      else tail = tail + v;
+    }
   }
   // Unrolled fast loop: compile-time slot J == k & 7 and a block-uniform phase PH (bit 0: the
   // sample is in [0, 128), bit 1: in [split, T)).  The accumulators start at 0, so 0 + v == v

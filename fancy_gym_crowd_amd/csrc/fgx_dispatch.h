@@ -59,13 +59,19 @@ inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave
 // k_episode or k_episode_w2: 5-link SimpleReacher without per-step info past one k_episode round
 // (two resident waves per SIMD, profiles/r02_w2_ab.jsonl); FGX_EPISODE_KERNEL=classic keeps k_episode
 inline bool w2_applies(const DevCfg& c, bool log) { return c.env == ENV_SIMPLE && c.nl == 5 && !log; }
-// k_episode_pair: 5-link HoleReacher without per-step info (two lanes per env, fgx_kernels.h);
-// FGX_EPISODE_KERNEL=classic keeps k_episode
+// k_episode_pair: 5-link HoleReacher without per-step info (two lanes per env, fgx_kernels.h) while
+// its 2N lanes fit one wave per SIMD (N <= 32768 on 256 CUs): each lane issues 15% fewer VALU
+// instructions than k_episode's (16384 / 32768 envs: 487 / 493 vs 517 / 525 us).  Past that the
+// pairs' second wave per SIMD does not pay for the duplicated plan / controller / dynamics work
+// (65536: 648 vs 530 us; profiles/r03_pair_scan.jsonl).  FGX_EPISODE_KERNEL=classic / =pair force.
 inline bool pair_applies(const DevCfg& c, bool log) { return c.env == ENV_HOLE && c.nl == 5 && !log; }
 inline int classic_choice(const DevCfg& c, bool log) {
   if (pair_applies(c, log)) {
-    const char* v = std::getenv("FGX_EPISODE_KERNEL");
-    return (v && std::strcmp(v, "classic") == 0) ? EK_CLASSIC : EK_PAIR;
+    if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
+      if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
+      if (std::strcmp(v, "pair") == 0) return EK_PAIR;
+    }
+    return 2 * c.N <= round_envs() ? EK_PAIR : EK_CLASSIC;
   }
   if (!w2_applies(c, log)) return EK_CLASSIC;
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {

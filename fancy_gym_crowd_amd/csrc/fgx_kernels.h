@@ -25,15 +25,16 @@ namespace fgx {
 // q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
 // fk0: FK is current for q (k_episode's epilogue), so cos / sin of q[0] are c[0] / s[0].
 // gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
-// s1: element stride of d1 (the per-step observations are component-major, [T, obs, N])
+// s1: element stride of d1 (the per-step observations are component-major, [T, obs, N]: d1 is then
+// the wave-uniform row of the sample and eo the env's element in it, info_st)
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
                                          bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
-                                         const double* gsn = nullptr, int64_t s1 = 1) {
+                                         const double* gsn = nullptr, int64_t s1 = 1, uint32_t eo = 0) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
-    if (d1) { if (s1 != 1) info_st(d1 + p * s1, x); else d1[p] = x; }
+    if (d1) { if (s1 != 1) info_st(d1, (uint32_t)(p * s1) + eo, x); else d1[p] = x; }
     if (d2) d2[p] = x;
     ++p;
   };
@@ -818,20 +819,27 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     const float fnan = __builtin_nanf("");
     float pp[NL], pv[NL];
     {
-      const int64_t ek = (int64_t)kk * N + e;        // [T, N] arrays
-      const int64_t ed = (int64_t)kk * NL * N + e;   // [T, dof, N] arrays: component d at ed + d N
+      // rows of the wave-uniform sample kk: [T, N] arrays at kk N, [T, X, N] at kk X N (info_st)
+      const int64_t r1 = (int64_t)kk * N, rd = (int64_t)kk * NL * N;
+      const uint32_t ue = (uint32_t)e, un = (uint32_t)N;
       if (o.positions && MP != MP_GIVEN) {
         gen.at(c, kk, pp, pv);
-        for (int d = 0; d < NL; ++d) { info_st(o.positions + ed + d * N, pp[d]); info_st(o.velocities + ed + d * N, pv[d]); }
+        for (int d = 0; d < NL; ++d) {
+          info_st(o.positions + rd, d * un + ue, pp[d]);
+          info_st(o.velocities + rd, d * un + ue, pv[d]);
+        }
       }
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) info_st(o.step_actions + ed + d * N, dnan);
-      if (o.step_rewards) info_st(o.step_rewards + ek, dnan);
+        for (int d = 0; d < NL; ++d) info_st(o.step_actions + rd, d * un + ue, dnan);
+      if (o.step_rewards) info_st(o.step_rewards + r1, ue, dnan);
       if (o.step_obs)
-        for (int q = 0; q < c.full_dim; ++q) info_st(o.step_obs + ((int64_t)kk * c.full_dim + q) * N + e, fnan);
-      if (o.is_collided) { info_st(o.is_collided + ek, (uint8_t)0); info_st(o.is_success + ek, (uint8_t)0); }
-      if (o.end_effector) { info_st(o.end_effector + 2 * kk * N + e, dnan); info_st(o.end_effector + (2 * kk + 1) * N + e, dnan); }
-      if (o.reward_dist) { info_st(o.reward_dist + ek, dnan); info_st(o.reward_ctrl + ek, dnan); }
+        for (int q = 0; q < c.full_dim; ++q) info_st(o.step_obs + (int64_t)kk * c.full_dim * N, q * un + ue, fnan);
+      if (o.is_collided) { info_st(o.is_collided + r1, ue, (uint8_t)0); info_st(o.is_success + r1, ue, (uint8_t)0); }
+      if (o.end_effector) {
+        info_st(o.end_effector + 2 * r1, ue, dnan);
+        info_st(o.end_effector + 2 * r1, un + ue, dnan);
+      }
+      if (o.reward_dist) { info_st(o.reward_dist + r1, ue, dnan); info_st(o.reward_ctrl + r1, ue, dnan); }
     }
   };
   auto pad_info = [&](int L, auto& gen) {
@@ -935,22 +943,27 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     if (LOG) {
       // the info arrays are time- and component-major ([T, N] / [T, X, N]): every store of a wave
       // covers 64 consecutive envs
-      const int64_t ek = (int64_t)k * N + e;
-      const int64_t ed = (int64_t)k * NL * N + e;
+      // k is wave-uniform in the logging loop: rows of sample k (info_st's SGPR bases)
+      const int ku = __builtin_amdgcn_readfirstlane(k);
+      const int64_t r1 = (int64_t)ku * N, rd = (int64_t)ku * NL * N;
+      const uint32_t ue = (uint32_t)e, un = (uint32_t)N;
       if (o.step_actions)
-        for (int d = 0; d < NL; ++d) info_st(o.step_actions + ed + d * N, a[d]);
+        for (int d = 0; d < NL; ++d) info_st(o.step_actions + rd, d * un + ue, a[d]);
       if (o.positions && MP != MP_GIVEN)
-        for (int d = 0; d < NL; ++d) { info_st(o.positions + ed + d * N, pos[d]); info_st(o.velocities + ed + d * N, vel[d]); }
-      if (o.step_rewards) info_st(o.step_rewards + ek, r.reward);
+        for (int d = 0; d < NL; ++d) {
+          info_st(o.positions + rd, d * un + ue, pos[d]);
+          info_st(o.velocities + rd, d * un + ue, vel[d]);
+        }
+      if (o.step_rewards) info_st(o.step_rewards + r1, ue, r.reward);
       // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
-      if (o.step_obs) emit_obs(c, v, false, o.step_obs + (int64_t)k * c.full_dim * N + e, nullptr, false, true,
-                               nullptr, nullptr, N);
+      if (o.step_obs) emit_obs(c, v, false, o.step_obs + (int64_t)ku * c.full_dim * N, nullptr, false, true,
+                               nullptr, nullptr, N, ue);
       if (ENV != ENV_SIMPLE) {
-        if (o.is_collided) { info_st(o.is_collided + ek, (uint8_t)r.coll); info_st(o.is_success + ek, (uint8_t)r.success); }
-        if (o.end_effector) { info_st(o.end_effector + 2 * k * N + e, v.jx[NL]); info_st(o.end_effector + (2 * k + 1) * N + e, v.jy[NL]); }
+        if (o.is_collided) { info_st(o.is_collided + r1, ue, (uint8_t)r.coll); info_st(o.is_success + r1, ue, (uint8_t)r.success); }
+        if (o.end_effector) { info_st(o.end_effector + 2 * r1, ue, v.jx[NL]); info_st(o.end_effector + 2 * r1, un + ue, v.jy[NL]); }
       } else if (o.reward_dist) {
-        info_st(o.reward_dist + ek, r.rdist);
-        info_st(o.reward_ctrl + ek, r.rctrl);
+        info_st(o.reward_dist + r1, ue, r.rdist);
+        info_st(o.reward_ctrl + r1, ue, r.rctrl);
       }
     }
     bool replan_now = (k == k_replan);

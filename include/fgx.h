@@ -175,6 +175,7 @@ typedef struct fgx_dims {
 /* Optional per-step outputs of fgx_step / fgx_step_traj (black_box_wrapper.py:185-249,
  * verbose >= 2).  Any pointer may be NULL.  Rows after trajectory_length are set to NaN (0 for the
  * u8 flags); positions / velocities hold the whole plan (NaN after a learned plan length).
+ * (Per-step arrays need n_envs < 2^24: FGX_E_UNSUPPORTED otherwise.)
  * The arrays are TIME- AND COMPONENT-MAJOR (ABI 7): [T, N] (sample k of env e at k*N + e) and
  * [T, X, N] (component x at (k*X + x)*N + e), so that a wave's per-step stores cover consecutive
  * envs; [N, T] / [N, T, X] are transposed / permuted views. */
