@@ -29,7 +29,7 @@ class FgxConfig(ctypes.Structure):
         "abi_version", "env_kind", "n_links", "random_start", "allow_self_collision",
         "allow_wall_collision", "mp_kind", "phase_kind", "n_basis", "zero_start", "zero_goal",
         "ctrl_kind", "T", "max_episode_steps", "replan_period", "max_planning_times",
-        "condition_on_desired", "time_aware", "return_context", "reserved0")] + [
+        "condition_on_desired", "time_aware", "return_context", "num_basis_outside")] + [
         (n, ctypes.c_double) for n in (
             "dt", "duration", "tau", "delay", "alpha_phase", "bandwidth", "weights_scale",
             "goal_scale", "alpha", "pc_length", "p_gain", "d_gain", "act_low", "act_high",

@@ -151,6 +151,9 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     if (c.T > 256) return fail(FGX_E_UNSUPPORTED, "plan length T > 256 not supported");
     if (c.n_basis < 1 || c.n_basis > kGenBasis) return fail(FGX_E_UNSUPPORTED, "n_basis must be in [1, 12]");
     if (c.n_basis + c.zero_start + c.zero_goal > kMaxBasis) return fail(FGX_E_INVALID, "too many basis functions");
+    // centres (j - o) / (n - 2o - 1) of the unbounded phase (fgx_tables.h rbf64): n - 2o - 1 >= 1
+    if (c.num_basis_outside < 0 || c.n_basis + c.zero_start + c.zero_goal - 2 * c.num_basis_outside - 1 < 1)
+      return fail(FGX_E_INVALID, "num_basis_outside must satisfy 0 <= o and num_basis - 2 o > 1");
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
       return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14
     if (!(c.tau > 0.0) || !(c.dt > 0.0) || !std::isfinite(c.tau)) return fail(FGX_E_INVALID, "tau/dt must be positive");
@@ -170,6 +173,7 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.nb = c.n_basis;
   d.zs = c.zero_start;
   d.zg = c.zero_goal;
+  d.nbo = c.num_basis_outside;
   d.ctrl = c.ctrl_kind;
   d.T = c.T;
   d.max_steps = c.max_episode_steps;
@@ -529,7 +533,7 @@ extern "C" int fgx_dbg_stamps(unsigned long long* host, int n) {
 }
 #endif
 
-// per-step info arrays are addressed with 32-bit byte offsets inside one sample's rows (info_st):
+// per-step info arrays: InfoStage keeps each row's per-sample stride in 32 bits (fgx_device.h):
 // N < 2^24 keeps kMaxObs rows of f64 below 4 GB (at 65536 envs the arrays are already 2.4 GB)
 static bool info_too_large(const Handle* h, const fgx_info* info) {
   return info && (info->positions || info->step_actions || info->step_obs || info->step_rewards || info->is_collided ||

@@ -40,7 +40,7 @@ enum : int { VALID_TAU = 1, VALID_DELAY = 2, VALID_POS = 4, INVALID_OBS_ZEROS = 
 struct DevCfg {
   int64_t N;
   int env, nl, random_start, allow_self, allow_wall;
-  int mp, phase, nb, zs, zg, ctrl, T, max_steps, replan /* do_replanning */, max_plans, cond_desired, time_aware,
+  int mp, phase, nb, zs, zg, nbo /* num_basis_outside */, ctrl, T, max_steps, replan /* do_replanning */, max_plans, cond_desired, time_aware,
       return_context;
   int obs_dim;      // full env observation (3n+3 simple, 3n+4 hole)
   int full_dim;     // obs_dim + time_aware
@@ -154,24 +154,164 @@ __device__ __forceinline__ void count_inner(long long* base, long long sum, bool
     atomicAdd((unsigned long long*)(base + (size_t)(w % kInnerSlots) * kInnerStride), (unsigned long long)sum);
 }
 
-// Stores into the per-step info arrays (write-once streams of up to GBs per BB step).  FGX_INFO_NT
-// (A/B build): non-temporal stores (round 3: +3% LongSimpleReacher, -11% HoleReacher; not used).
-// row: the array's block of one wave-uniform sample index (k * X * N), idx: the lane's element in it
-// (component * N + env).  The row address is made an SGPR value and the element a 32-bit offset, so
-// the store takes global_store's saddr form: no per-store 64-bit VGPR address arithmetic (fgx_step
-// rejects per-step arrays for N >= 2^24, where 32-bit byte offsets could overflow).
-template <typename T>
-__device__ __forceinline__ void info_st(T* row, uint32_t idx, T x) {
-  const uint64_t a = (uint64_t)row;
-  const uint64_t ua = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  T* p = (T*)((char*)ua + (uint64_t)(idx * (uint32_t)sizeof(T)));
-#ifdef FGX_INFO_NT
-  __builtin_nontemporal_store(x, p);
-#else
-  *p = x;
-#endif
+// orders this wave's LDS writes before its later reads (and reads before later writes): LDS
+// operations of one wave execute in order, so the compiler's ordering is all that is needed
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// ------------------------------------------------------------------ wave write-combining of info rows
+// The logging k_episode writes the verbose-2 per-step arrays ([T, N] / [T, X, N], up to GBs per BB
+// step).  One dword store per lane and row puts 256 B (f32) in flight per wave instruction; a lone
+// wave per SIMD then holds too few bytes in flight against the write latency of a GB-sized stream.
+// InfoStage collects the wave's values of one sample (every row of every array) in the wave's LDS
+// region, one slot of 64 lanes per row, and writes them back transposed: each lane stores 16
+// contiguous bytes (4 f32 / 2 f64 / 4 u8 envs), so one store instruction covers 4 f32 rows (or 2
+// f64 rows) of 64 envs = 1 KiB.  Slots: f32 [positions NL | velocities NL | step_obs full_dim],
+// f64 [step_actions NL | step_rewards | end_effector x, y | reward_dist | reward_ctrl], u8
+// [is_collided | is_success].  Per slot the table holds the address of the wave's first env in the
+// row of sample 0 and the row stride per sample (bytes).
+__host__ __device__ inline int stage_n32(int nl, int full_dim) { return 2 * nl + full_dim; }
+__host__ __device__ inline int stage_n64(int nl) { return nl + 5; }
+__host__ __device__ inline size_t stage_wave_bytes(int nl, int full_dim) {
+  const int n32 = stage_n32(nl, full_dim), n64 = stage_n64(nl);
+  return (size_t)n64 * 512 + (size_t)n32 * 256 + 128 + (size_t)(n32 + n64 + 2) * 16;
+}
+__host__ __device__ inline size_t stage_tab_offset(size_t tab_floats) { return (tab_floats * 4 + 15) & ~(size_t)15; }
+
+template <int NL>
+struct InfoStage {
+  static constexpr int N64 = NL + 5;
+  double* d;       // [N64][64]
+  float* f;        // [n32][64]
+  uint8_t* b;      // [2][64]
+  uint64_t* tab;   // [slot][2]: base, stride (bytes)
+  int lane, n32, nval, n4;
+  bool any;        // some info array is written
+
+  // region: the block's staging area (after the basis table); e: the lane's env (< N)
+  __device__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan_rows) {
+    lane = (int)(threadIdx.x & 63);
+    n32 = stage_n32(NL, c.full_dim);
+    char* w = region + (size_t)(threadIdx.x >> 6) * stage_wave_bytes(NL, c.full_dim);
+    d = (double*)w;
+    f = (float*)(w + N64 * 512);
+    b = (uint8_t*)(w + N64 * 512 + n32 * 256);
+    tab = (uint64_t*)(w + N64 * 512 + n32 * 256 + 128);
+    const int64_t N = c.N, e0 = e - lane;
+    nval = (int)min((int64_t)64, N - e0);
+    n4 = (int)(N & 3);
+    any = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector ||
+          o.reward_dist;
+    const int ns = n32 + N64 + 2;
+    // (lanes nval..63 of a partial last wave have left the kernel: the active lanes 0..nval-1 fill
+    // every entry)
+    for (int s = lane; s < ns; s += nval) {
+      const char* base = nullptr;
+      uint64_t ks = 0;
+      if (s < n32) {
+        if (s < 2 * NL) {
+          const float* a = (s < NL) ? o.positions : o.velocities;
+          if (a && plan_rows) base = (const char*)(a + (s % NL) * N + e0);
+          ks = (uint64_t)NL * N * 4;
+        } else {
+          if (o.step_obs) base = (const char*)(o.step_obs + (s - 2 * NL) * N + e0);
+          ks = (uint64_t)c.full_dim * N * 4;
+        }
+      } else if (s < n32 + N64) {
+        const int t = s - n32;
+        if (t < NL) {
+          if (o.step_actions) base = (const char*)(o.step_actions + t * N + e0);
+          ks = (uint64_t)NL * N * 8;
+        } else if (t == NL) {
+          if (o.step_rewards) base = (const char*)(o.step_rewards + e0);
+          ks = (uint64_t)N * 8;
+        } else if (t <= NL + 2) {
+          if (o.end_effector) base = (const char*)(o.end_effector + (t - NL - 1) * N + e0);
+          ks = (uint64_t)2 * N * 8;
+        } else {
+          const double* a = (t == NL + 3) ? o.reward_dist : o.reward_ctrl;
+          if (a) base = (const char*)(a + e0);
+          ks = (uint64_t)N * 8;
+        }
+      } else {
+        const uint8_t* a = (s == n32 + N64) ? o.is_collided : o.is_success;
+        if (a) base = (const char*)(a + e0);
+        ks = (uint64_t)N;
+      }
+      tab[2 * s] = (uint64_t)base;
+      tab[2 * s + 1] = ks;
+    }
+    wave_lds_sync();
+  }
+  // the lane's value of slot s of the current sample
+  __device__ __forceinline__ void pos(int dd, float x) { f[dd * 64 + lane] = x; }
+  __device__ __forceinline__ void vel(int dd, float x) { f[(NL + dd) * 64 + lane] = x; }
+  __device__ __forceinline__ float* obs_row() { return f + 2 * NL * 64 + lane; }   // element stride 64
+  __device__ __forceinline__ void act(int dd, double x) { d[dd * 64 + lane] = x; }
+  __device__ __forceinline__ void rew(double x) { d[NL * 64 + lane] = x; }
+  __device__ __forceinline__ void ee(double x, double y) { d[(NL + 1) * 64 + lane] = x; d[(NL + 2) * 64 + lane] = y; }
+  __device__ __forceinline__ void rdc(double x, double y) { d[(NL + 3) * 64 + lane] = x; d[(NL + 4) * 64 + lane] = y; }
+  __device__ __forceinline__ void flags(uint8_t x, uint8_t y) { b[lane] = x; b[64 + lane] = y; }
+
+  // write the staged rows of sample kk (wave-uniform); every lane of the wave's envs active.  A full
+  // wave (64 envs, 16-B aligned rows: N % 4 == 0) stores transposed 16-B pieces; otherwise (the
+  // partial last wave, whose lanes past N have left the kernel, or N % 4 != 0) every lane stores its
+  // own element of each row.
+  __device__ void flush(int kk) {
+    if (!any) return;
+    wave_lds_sync();
+    const uint32_t k = (uint32_t)kk;
+    if (nval == 64 && n4 == 0) {
+      {   // f32: 4 slots per instruction, lane = (slot within the group, 4-env quad)
+        const int q = lane & 15;
+        for (int g = 0; g < n32; g += 4) {
+          const int s = g + (lane >> 4);
+          if (s >= n32) continue;
+          const uint64_t base = tab[2 * s];
+          if (!base) continue;
+          const float4 x = *(const float4*)(f + s * 64 + 4 * q);
+          *(float4*)((float*)(base + (uint64_t)k * (uint32_t)tab[2 * s + 1]) + 4 * q) = x;
+        }
+      }
+      {   // f64: 2 slots per instruction, lane = (slot within the group, env pair)
+        const int q = lane & 31;
+        for (int g = 0; g < N64; g += 2) {
+          const int s = g + (lane >> 5);
+          if (s >= N64) continue;
+          const uint64_t base = tab[2 * (n32 + s)];
+          if (!base) continue;
+          const double2 x = *(const double2*)(d + s * 64 + 2 * q);
+          *(double2*)((double*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + s) + 1]) + 2 * q) = x;
+        }
+      }
+      if (lane < 32) {   // u8: lanes 0-15 is_collided, 16-31 is_success, 4 envs each
+        const int s = lane >> 4, q = lane & 15;
+        const uint64_t base = tab[2 * (n32 + N64 + s)];
+        if (base) {
+          const uint32_t x = *(const uint32_t*)(b + s * 64 + 4 * q);
+          *(uint32_t*)((uint8_t*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + N64 + s) + 1]) + 4 * q) = x;
+        }
+      }
+    } else {
+      for (int s = 0; s < n32; ++s) {
+        const uint64_t base = tab[2 * s];
+        if (base) ((float*)(base + (uint64_t)k * (uint32_t)tab[2 * s + 1]))[lane] = f[s * 64 + lane];
+      }
+      for (int s = 0; s < N64; ++s) {
+        const uint64_t base = tab[2 * (n32 + s)];
+        if (base) ((double*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + s) + 1]))[lane] = d[s * 64 + lane];
+      }
+      for (int s = 0; s < 2; ++s) {
+        const uint64_t base = tab[2 * (n32 + N64 + s)];
+        if (base) ((uint8_t*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + N64 + s) + 1]))[lane] = b[s * 64 + lane];
+      }
+    }
+    wave_lds_sync();
+  }
+};
 
 // ------------------------------------------------------------------ wave reductions (all 64 lanes active)
 __device__ __forceinline__ int wave_min(int x) {

@@ -183,9 +183,18 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
       return 0;
     }
   }
-  if (log)
-    hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), lds, stream, c, s,
+  if (log) {
+    // + the four waves' info staging regions (InfoStage, fgx_device.h)
+    const size_t ll = stage_tab_offset(lds / sizeof(float)) + (threads / 64) * stage_wave_bytes(NL, c.full_dim);
+    if (ll > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k_episode<ENV, MP, CTRL, NL, NB, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll) != hipSuccess) {
+      err = "k_episode (info rows): cannot raise the dynamic LDS limit";
+      return -2;
+    }
+    hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), ll, stream, c, s,
                        params, dpos, dvel, o);
+  }
   else
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, false>), dim3(blocks), dim3(threads), lds, stream, c, s,
                        params, dpos, dvel, o);

@@ -60,14 +60,6 @@ struct JlShape {
   }
 };
 
-// orders this wave's LDS writes before its later reads (and reads before later writes): LDS
-// operations of one wave execute in order, so the compiler's ordering is all that is needed
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int MP, int NL, int NB>
 // gw: envs per wave actually used (<= G; experiments, FGX_JL_GW); LDS slots keep the compile-time
 // stride G

@@ -25,16 +25,16 @@ namespace fgx {
 // q0 are FK's c[0] / s[0] (the same sincos of the same angle) and those of +0 are exactly 1 / +0.
 // fk0: FK is current for q (k_episode's epilogue), so cos / sin of q[0] are c[0] / s[0].
 // gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
-// s1: element stride of d1 (the per-step observations are component-major, [T, obs, N]: d1 is then
-// the wave-uniform row of the sample and eo the env's element in it, info_st)
+// s1: element stride of d1 (the per-step observations: the lane's column of the wave's LDS staging
+// slots, stride 64, InfoStage)
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
                                          bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
-                                         const double* gsn = nullptr, int64_t s1 = 1, uint32_t eo = 0) {
+                                         const double* gsn = nullptr, int s1 = 1) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
-    if (d1) { if (s1 != 1) info_st(d1, (uint32_t)(p * s1) + eo, x); else d1[p] = x; }
+    if (d1) d1[p * s1] = x;
     if (d2) d2[p] = x;
     ++p;
   };
@@ -812,47 +812,38 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   const int Te = (MP == MP_GIVEN && s.plan_len) ? s.plan_len[e] : c.T;
   // the per-step info rows L..T-1: the full desired plan (black_box_wrapper.py:245-246), NaN (0 for
   // the flags) in the per-step arrays after trajectory_length; gen: the plan's generator at sample L.
-  // The wave walks the rows together from its smallest L (lanes idle below their own), so every
-  // store instruction covers one row of the [T, X, N] arrays: consecutive envs, not X lines per lane.
+  // The wave walks the rows together (lanes whose env has stopped pad their row beside the running
+  // ones) and the staged rows of each sample leave the wave as wide stores (InfoStage::flush).
+  InfoStage<NL> ist;
+  if constexpr (LOG) {
+    const size_t tabf = (MP == MP_GIVEN) ? 0 : (size_t)c.rows * c.stride;
+    ist.init(c, o, (char*)lds_tab + stage_tab_offset(tabf), e, MP != MP_GIVEN);
+  }
   auto pad_row = [&](int kk, auto& gen) {
     const double dnan = __builtin_nan("");
     const float fnan = __builtin_nanf("");
-    float pp[NL], pv[NL];
-    {
-      // rows of the wave-uniform sample kk: [T, N] arrays at kk N, [T, X, N] at kk X N (info_st)
-      const int64_t r1 = (int64_t)kk * N, rd = (int64_t)kk * NL * N;
-      const uint32_t ue = (uint32_t)e, un = (uint32_t)N;
-      if (o.positions && MP != MP_GIVEN) {
-        gen.at(c, kk, pp, pv);
-        for (int d = 0; d < NL; ++d) {
-          info_st(o.positions + rd, d * un + ue, pp[d]);
-          info_st(o.velocities + rd, d * un + ue, pv[d]);
-        }
-      }
-      if (o.step_actions)
-        for (int d = 0; d < NL; ++d) info_st(o.step_actions + rd, d * un + ue, dnan);
-      if (o.step_rewards) info_st(o.step_rewards + r1, ue, dnan);
-      if (o.step_obs)
-        for (int q = 0; q < c.full_dim; ++q) info_st(o.step_obs + (int64_t)kk * c.full_dim * N, q * un + ue, fnan);
-      if (o.is_collided) { info_st(o.is_collided + r1, ue, (uint8_t)0); info_st(o.is_success + r1, ue, (uint8_t)0); }
-      if (o.end_effector) {
-        info_st(o.end_effector + 2 * r1, ue, dnan);
-        info_st(o.end_effector + 2 * r1, un + ue, dnan);
-      }
-      if (o.reward_dist) { info_st(o.reward_dist + r1, ue, dnan); info_st(o.reward_ctrl + r1, ue, dnan); }
+    if (o.positions && MP != MP_GIVEN) {
+      float pp[NL], pv[NL];
+      gen.at(c, kk, pp, pv);
+#pragma unroll
+      for (int d = 0; d < NL; ++d) { ist.pos(d, pp[d]); ist.vel(d, pv[d]); }
     }
+#pragma unroll
+    for (int d = 0; d < NL; ++d) ist.act(d, dnan);
+    ist.rew(dnan);
+    float* so = ist.obs_row();
+    for (int q = 0; q < c.full_dim; ++q) so[q * 64] = fnan;
+    ist.flags(0, 0);
+    ist.ee(dnan, dnan);
+    ist.rdc(dnan, dnan);
   };
-  auto pad_info = [&](int L, auto& gen) {
-    for (int kk = wave_min_active(min(L, c.T)); kk < c.T; ++kk)
-      if (kk >= L) pad_row(kk, gen);
-  };
-  if constexpr (LOG) {   // trajectory validity (the logging instantiation serves valid_flags != 0)
-    if (c.valid_flags &&
-        !plan_valid<MP, NL>(c, tg, params ? params + e * c.n_params : nullptr, dpos, e, Te)) {
-      pad_info(0, tg);
-      invalid_transition(c, s, o, e, v);
-      return;
-    }
+  // trajectory validity (the logging instantiation serves valid_flags != 0): an invalid plan takes
+  // no env step; its lane pads every row in the sample loop below (L = 0), then makes the artificial
+  // transition instead of the epilogue
+  bool invalid = false;
+  if constexpr (LOG) {
+    if (c.valid_flags)
+      invalid = !plan_valid<MP, NL>(c, tg, params ? params + e * c.n_params : nullptr, dpos, e, Te);
   }
   int split = 0;
   if (ENV == ENV_SIMPLE && !c.sched_state) {
@@ -939,31 +930,22 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
       ps.add(k, r.reward, split);
       if (rew_row) rew_row[(int64_t)k * N] = r.reward;
     }
-    // ---- info (verbose >= 2, black_box_wrapper.py:220-227)
-    if (LOG) {
-      // the info arrays are time- and component-major ([T, N] / [T, X, N]): every store of a wave
-      // covers 64 consecutive envs
-      // k is wave-uniform in the logging loop: rows of sample k (info_st's SGPR bases)
-      const int ku = __builtin_amdgcn_readfirstlane(k);
-      const int64_t r1 = (int64_t)ku * N, rd = (int64_t)ku * NL * N;
-      const uint32_t ue = (uint32_t)e, un = (uint32_t)N;
-      if (o.step_actions)
-        for (int d = 0; d < NL; ++d) info_st(o.step_actions + rd, d * un + ue, a[d]);
-      if (o.positions && MP != MP_GIVEN)
-        for (int d = 0; d < NL; ++d) {
-          info_st(o.positions + rd, d * un + ue, pos[d]);
-          info_st(o.velocities + rd, d * un + ue, vel[d]);
-        }
-      if (o.step_rewards) info_st(o.step_rewards + r1, ue, r.reward);
+    // ---- info (verbose >= 2, black_box_wrapper.py:220-227): the sample's values into the wave's
+    // staging slots (flushed as wide stores once the wave has reconverged, InfoStage)
+    if constexpr (LOG) {
+#pragma unroll
+      for (int d = 0; d < NL; ++d) ist.act(d, a[d]);
+      if (MP != MP_GIVEN)
+#pragma unroll
+        for (int d = 0; d < NL; ++d) { ist.pos(d, pos[d]); ist.vel(d, vel[d]); }
+      ist.rew(r.reward);
       // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
-      if (o.step_obs) emit_obs(c, v, false, o.step_obs + (int64_t)ku * c.full_dim * N, nullptr, false, true,
-                               nullptr, nullptr, N, ue);
+      if (o.step_obs) emit_obs(c, v, false, ist.obs_row(), nullptr, false, true, nullptr, nullptr, 64);
       if (ENV != ENV_SIMPLE) {
-        if (o.is_collided) { info_st(o.is_collided + r1, ue, (uint8_t)r.coll); info_st(o.is_success + r1, ue, (uint8_t)r.success); }
-        if (o.end_effector) { info_st(o.end_effector + 2 * r1, ue, v.jx[NL]); info_st(o.end_effector + 2 * r1, un + ue, v.jy[NL]); }
-      } else if (o.reward_dist) {
-        info_st(o.reward_dist + r1, ue, r.rdist);
-        info_st(o.reward_ctrl + r1, ue, r.rctrl);
+        ist.flags((uint8_t)r.coll, (uint8_t)r.success);
+        ist.ee(v.jx[NL], v.jy[NL]);
+      } else {
+        ist.rdc(r.rdist, r.rctrl);
       }
     }
     bool replan_now = (k == k_replan);
@@ -1209,6 +1191,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     // the wave walks the plan rows together (k is wave-uniform here: no fast blocks with LOG): a
     // lane whose env has stopped pads its row k beside the samples of the lanes still running, so
     // every info store covers the wave's consecutive envs in one row, then rows k..T-1 of all lanes
+    stop = invalid;
     for (;; ++k) {
       const bool act = !stop && k < Te;
       if (__ballot(act) == 0) break;
@@ -1218,9 +1201,17 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
         L = min(L, k);
         if (k < c.T) pad_row(k, tg);
       }
+      if (k < c.T) ist.flush(__builtin_amdgcn_readfirstlane(k));
     }
     L = min(L, k);
-    pad_info(k, tg);
+    for (int kk = __builtin_amdgcn_readfirstlane(k); kk < c.T; ++kk) {
+      pad_row(kk, tg);
+      ist.flush(kk);
+    }
+    if (invalid) {
+      invalid_transition(c, s, o, e, v);
+      return;
+    }
   } else {
     while (!stop && k < Te) {
       stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, c.sched_state);

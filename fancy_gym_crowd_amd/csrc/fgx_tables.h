@@ -15,12 +15,14 @@ __device__ inline double phase64(const DevCfg& c, double t, double tau, double d
   return exp((-alpha_x) * lin);
 }
 
-// normalized RBF at phase x, f64, all n = nb + zs + zg columns (oracle/mp.py:rbf64)
+// normalized RBF at phase x, f64, all n = nb + zs + zg columns (oracle/mp.py:rbf64); centres at the
+// unbounded phase of linspace(delay - o d, delay + tau + o d, n), d = tau / (n - 2o - 1), i.e. linear
+// phase u_j = (j - o) / (n - 2o - 1) (o = num_basis_outside; 0: j / (n - 1))
 __device__ inline void rbf64(const DevCfg& c, double alpha_x, double bw, double x, double* phi) {
   const int n = c.nb + c.zs + c.zg;
   double cen[kMaxBasis + 4], e[kMaxBasis + 4];
   for (int j = 0; j < n; ++j) {
-    const double u = (n > 1) ? (double)j / (double)(n - 1) : 0.0;
+    const double u = (n > 1) ? (double)(j - c.nbo) / (double)(n - 2 * c.nbo - 1) : 0.0;
     cen[j] = (c.phase == 0) ? u : exp((-alpha_x) * u);
   }
   for (int j = 0; j < n; ++j) {

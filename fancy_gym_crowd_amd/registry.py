@@ -500,8 +500,14 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c.n_basis = int(bs.get('num_basis', 10))
     c.zero_start = int(bs.get('num_basis_zero_start', D['num_basis_zero_start'])) if bs_type == 'zero_rbf' else 0
     c.zero_goal = int(bs.get('num_basis_zero_goal', D['num_basis_zero_goal'])) if bs_type == 'zero_rbf' else 0
-    if int(bs.get('num_basis_outside', 0)) != 0:
-        raise NotImplementedError("num_basis_outside != 0")
+    # num_basis_outside (mp_pytorch NormalizedRBF / ProDMP basis generators): centres beyond the
+    # phase's [0, 1]; the zero-padding generator takes no such argument
+    c.num_basis_outside = int(bs.get('num_basis_outside', 0))
+    if c.num_basis_outside and bs_type == 'zero_rbf':
+        raise TypeError("ZeroPaddingNormalizedRBFBasisGenerator got an unexpected keyword argument "
+                        "'num_basis_outside'")
+    if c.num_basis_outside < 0 or c.n_basis - 2 * c.num_basis_outside - 1 < 1:
+        raise ValueError("num_basis_outside must satisfy 0 <= o and num_basis - 2 o > 1")
     c.bandwidth = float(bs.get('basis_bandwidth_factor', D['basis_bandwidth_factor']))
     c.tau = float(tau)
     c.delay = float(ph.get('delay', D['delay']))

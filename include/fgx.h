@@ -124,7 +124,8 @@ typedef struct fgx_config {
   int32_t condition_on_desired; /* black_box_wrapper.py:235-237                             */
   int32_t time_aware;           /* TimeAwareObservation appended (utils/wrappers.py:49-63)  */
   int32_t return_context;       /* context-mask the BB observation (black_box_wrapper.py:90-95) */
-  int32_t reserved0;
+  int32_t num_basis_outside;    /* RBF centres beyond [0, 1] of the phase on each side (mp_pytorch
+                                   NormalizedRBF / ProDMP num_basis_outside; was reserved0 = 0) */
   double dt;                    /* env dt (base_reacher.py:21)                              */
   double duration;              /* BB duration (make_env_helpers.py:110-111)                */
   double tau, delay, alpha_phase; /* phase generator                                        */

@@ -15,7 +15,8 @@ time grid   absolute step index i >= 0, t_i = i*dt (f64); a plan that starts at 
             set_duration(duration, dt) -> T = round(duration/dt) samples after t0]
 phase       linear: x = clip((t-delay)/tau, 0, 1); exp: x = exp(-alpha_x * max(t-delay, 0)/tau)
             [factory/phase_generator_factory.py:11-14]
-basis       normalized RBF, centres = phase of linspace(delay, delay+tau, n), bandwidth
+basis       normalized RBF, centres = unbounded phase of linspace(delay - o d, delay + tau + o d, n),
+            d = tau / (n - 2o - 1), o = num_basis_outside (default 0), bandwidth
             h_j = bw / (c_{j+1}-c_j)^2 (last repeated), phi_j = exp(-h_j (x-c_j)^2 / 2) / sum;
             zero padding builds n_b + z_s + z_g RBFs and keeps columns z_s..z_s+n_b-1
             [factory/basis_generator_factory.py:10-17]
@@ -55,6 +56,7 @@ class MPSpec:
     bandwidth: float = 3.0
     zero_start: int = 0
     zero_goal: int = 0
+    basis_outside: int = 0         # num_basis_outside (centres beyond the phase's [0, 1])
     weights_scale: float = 1.0
     goal_scale: float = 1.0
     alpha: float = 25.0            # DMP / ProDMP spring constant
@@ -85,7 +87,9 @@ def phase64(spec, t):
 
 def centers64(spec):
     n = spec.n_basis + spec.zero_start + spec.zero_goal
-    u = np.arange(n, dtype=np.float64) / (n - 1) if n > 1 else np.zeros(1)
+    o = spec.basis_outside                # centres at the unbounded phase of
+    # linspace(delay - o d, delay + tau + o d, n), d = tau / (n - 2o - 1): u_j = (j - o) / (n - 2o - 1)
+    u = (np.arange(n, dtype=np.float64) - o) / (n - 2 * o - 1) if n > 1 else np.zeros(1)
     c = u if spec.phase == "linear" else np.exp(-spec.alpha_phase * u)
     if n > 1:
         d = np.empty(n)

@@ -1,0 +1,68 @@
+"""The verbose-2 per-step info arrays row by row (black_box_wrapper.py:184-189,218-227,244-249),
+written by the logging k_episode through the wave's LDS staging slots (InfoStage, fgx_device.h).
+
+Every element of every array is checked, not only the rows before trajectory_length: rows < L
+against the oracle, rows >= L as the host contract states (NaN; 0 for the flags), the desired plan
+(positions / velocities) in full.  The batch sizes cover full waves, a partial last wave with
+N % 4 == 0 and one with N % 4 != 0 (the element-wise tail of InfoStage::flush).
+"""
+import numpy as np
+import pytest
+import torch
+
+import fancy_gym_crowd_amd as fgx
+from oracle import batched
+from test_gpu_parity import NAME, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+CASES = [
+    ("fancy_ProMP/LongSimpleReacher-v0", None),
+    ("fancy_ProDMP/HoleReacher-v0", None),
+    ("fancy_DMP/HoleReacher-v0", {"controller_kwargs": {"controller_type": "velocity"}}),
+    ("fancy_ProDMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}),
+]
+
+
+def _rows(dev, ref, L, name, T):
+    """rows < L equal the oracle's, rows >= L are the padding (NaN, 0 for the u8 flags)"""
+    d = np_(dev[name]).astype(np.float64)
+    r = np.asarray(ref[name], np.float64)
+    live = np.arange(T)[None, :] < L[:, None]
+    close(d[live], r[live])
+    pad = d[~live]
+    if name in ("is_collided", "is_success"):
+        assert (pad == 0).all(), name
+    else:
+        assert np.isnan(pad).all(), name
+
+
+@pytest.mark.parametrize("N", [256, 1000, 203])
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_info_rows_vs_oracle(ci, N):
+    env_id, over = CASES[ci]
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
+    assert env.episode_kernel(info_level=2) == "k_episode"
+    spec = spec_of(env)
+    tabs = split_tables(spec, np_(env.tables()))
+    ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=2, tables=tabs,
+                           **oracle_kwargs(env))
+    env.reset(seed=500)
+    ob.reset(seed=500)
+    rng = np.random.default_rng(ci * 1000 + N)
+    for _ in range(2):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        _, _, _, _, info = env.step(torch.from_numpy(params).to(DEV))
+        _, _, _, _, r_info = ob.step(params)
+        L = r_info["trajectory_length"]
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), L)
+        T = env.T
+        np.testing.assert_array_equal(np_(info["positions"]), r_info["positions"])
+        np.testing.assert_array_equal(np_(info["velocities"]), r_info["velocities"])
+        for name in ("step_actions", "step_observations", "step_rewards"):
+            _rows(info, r_info, L, name, T)
+        keys = ("is_collided", "is_success", "end_effector") if "is_collided" in info else ("reward_dist",
+                                                                                         "reward_ctrl")
+        for name in keys:
+            _rows(info, r_info, L, name, T)

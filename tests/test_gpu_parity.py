@@ -42,7 +42,7 @@ def spec_of(env):
     kind = {1: "promp", 2: "dmp", 3: "prodmp"}[c.mp_kind]
     return mp.MPSpec(kind=kind, dof=c.n_links, n_basis=c.n_basis, phase="linear" if c.phase_kind == 0 else "exp",
                      tau=c.tau, delay=c.delay, alpha_phase=c.alpha_phase, bandwidth=c.bandwidth,
-                     zero_start=c.zero_start, zero_goal=c.zero_goal, weights_scale=c.weights_scale,
+                     zero_start=c.zero_start, zero_goal=c.zero_goal, basis_outside=c.num_basis_outside, weights_scale=c.weights_scale,
                      goal_scale=c.goal_scale, alpha=c.alpha, pc_length=c.pc_length, dt=c.dt, duration=c.duration)
 
 

@@ -224,3 +224,28 @@ def test_register_gymnasium_with_stand_in():
         import gymnasium  # noqa: F401
     except ImportError:
         assert fgx.register_gymnasium() is False
+
+
+def test_num_basis_outside_resolution():
+    """basis_generator_kwargs num_basis_outside (mp_pytorch NormalizedRBF / ProDMP generators)."""
+    c, _ = fgx.resolve("fancy_DMP/SimpleReacher-v0", {"basis_generator_kwargs": {"num_basis_outside": 1}})
+    assert c.num_basis_outside == 1
+    c, _ = fgx.resolve("fancy_ProDMP/HoleReacher-v0")
+    assert c.num_basis_outside == 0
+    with pytest.raises(ValueError):   # num_basis - 2 o - 1 must stay >= 1
+        fgx.resolve("fancy_DMP/SimpleReacher-v0", {"basis_generator_kwargs": {"num_basis_outside": 2}})
+    with pytest.raises(TypeError):    # the zero-padding generator has no such argument
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", {"basis_generator_kwargs": {"num_basis_outside": 1}})
+
+
+def test_oracle_centres_with_basis_outside():
+    """centres = unbounded phase of linspace(-o d, tau + o d, n), d = tau / (n - 2o - 1)"""
+    from oracle import mp
+    for phase in ("linear", "exp"):
+        s = mp.MPSpec("dmp", 2, 7, phase, 2.0, basis_outside=2, alpha_phase=3.0)
+        c, _ = mp.centers64(s)
+        d = 2.0 / (7 - 4 - 1)
+        u = np.linspace(-2 * d, 2.0 + 2 * d, 7) / 2.0
+        np.testing.assert_allclose(c, u if phase == "linear" else np.exp(-3.0 * u), rtol=1e-15)
+        c0, _ = mp.centers64(mp.replace(s, basis_outside=0))
+        np.testing.assert_array_equal(c0, mp.centers64(mp.MPSpec("dmp", 2, 7, phase, 2.0, alpha_phase=3.0))[0])
