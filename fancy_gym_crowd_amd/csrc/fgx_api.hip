@@ -52,6 +52,7 @@ struct Handle {
   float* plan_vel = nullptr;
   int32_t* plan_len = nullptr;
   void* learned_block = nullptr;
+  double* obs_scratch = nullptr;   // info_level 2, SimpleReacher: qlog [T][nl][N] + gsave [2][N]
   bool learned() const { return dc.learn_tau || dc.learn_delay; }
 };
 
@@ -466,6 +467,7 @@ int fgx_destroy(void* handle) {
   if (h->state_block) (void)hipFree(h->state_block);
   if (h->learned_block) (void)hipFree(h->learned_block);
   if (h->scratch) (void)hipFree(h->scratch);
+  if (h->obs_scratch) (void)hipFree(h->obs_scratch);
   delete h;
   return FGX_OK;
 }
@@ -540,6 +542,24 @@ static bool info_too_large(const Handle* h, const fgx_info* info) {
                   info->end_effector || info->reward_dist) && h->dc.N >= (int64_t(1) << 24);
 }
 
+// info_level 2 (per-step observations) on SimpleReacher: the logging k_episode logs q per sample and
+// k_info_obs derives the trigonometric observation components from it (fgx_kernels.h); the handle's
+// scratch for that is allocated on the first such step (T * n_links * N + 2 N doubles)
+static int attach_obs_scratch(Handle* h, Outputs& o) {
+  if (!o.step_obs || h->dc.env != ENV_SIMPLE) return FGX_OK;
+  const size_t nq = (size_t)h->dc.T * h->dc.nl * h->dc.N;
+  if (!h->obs_scratch) {
+    const hipError_t e = hipMalloc(&h->obs_scratch, sizeof(double) * (nq + 2 * (size_t)h->dc.N));
+    if (e != hipSuccess) {
+      h->obs_scratch = nullptr;
+      return fail(FGX_E_NOMEM, std::string("hipMalloc per-step observation scratch: ") + hipGetErrorString(e));
+    }
+  }
+  o.qlog = h->obs_scratch;
+  o.gsave = h->obs_scratch + nq;
+  return FGX_OK;
+}
+
 int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t* terminated, uint8_t* truncated,
              int32_t* traj_len, float* final_obs, const fgx_info* info, int32_t autoreset, void* stream) {
   Handle* h = (Handle*)handle;
@@ -554,6 +574,7 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
+  if (const int rc = attach_obs_scratch(h, o)) return rc;
   if (h->learned()) {
     // per-env plans first (and, when requested, the time-major info copies), then the episode
     // over the given plans with per-env lengths
@@ -586,6 +607,7 @@ int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, floa
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
+  if (const int rc = attach_obs_scratch(h, o)) return rc;
   o.positions = nullptr;
   o.velocities = nullptr;   // the caller already holds the desired trajectories
   return launch_episode(*h, MP_GIVEN, nullptr, des_pos, des_vel, o, (hipStream_t)stream);

@@ -123,6 +123,11 @@ struct Outputs {
   double* reward_dist;
   double* reward_ctrl;
   long long* inner_steps;
+  // info_level 2, SimpleReacher: the logging k_episode leaves the trigonometric and end-effector
+  // components of the per-step observations to k_info_obs; it logs q per sample ([T][NL][N] f64) and
+  // the episode's goal ([2][N] f64, before the auto-reset) for it (handle scratch, fgx_api.hip)
+  double* qlog;
+  double* gsave;
   int autoreset;
 #ifdef FGX_STAMPS
   unsigned long long* stamps;   // diagnostics build only: per-wave section clocks (tools/stamps.py)
@@ -170,11 +175,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // region, one slot of 64 lanes per row, and writes them back transposed: each lane stores 16
 // contiguous bytes (4 f32 / 2 f64 / 4 u8 envs), so one store instruction covers 4 f32 rows (or 2
 // f64 rows) of 64 envs = 1 KiB.  Slots: f32 [positions NL | velocities NL | step_obs full_dim],
-// f64 [step_actions NL | step_rewards | end_effector x, y | reward_dist | reward_ctrl], u8
-// [is_collided | is_success].  Per slot the table holds the address of the wave's first env in the
+// f64 [step_actions NL | step_rewards | end_effector x, y | reward_dist | reward_ctrl | q NL (qlog)],
+// u8 [is_collided | is_success].  With qlog (defer) the step_obs slots k_info_obs writes (cos / sin
+// of q, end effector - goal) have no row here.  Per slot the table holds the address of the wave's first env in the
 // row of sample 0 and the row stride per sample (bytes).
 __host__ __device__ inline int stage_n32(int nl, int full_dim) { return 2 * nl + full_dim; }
-__host__ __device__ inline int stage_n64(int nl) { return nl + 5; }
+__host__ __device__ inline int stage_n64(int nl) { return 2 * nl + 5; }
 __host__ __device__ inline size_t stage_wave_bytes(int nl, int full_dim) {
   const int n32 = stage_n32(nl, full_dim), n64 = stage_n64(nl);
   return (size_t)n64 * 512 + (size_t)n32 * 256 + 128 + (size_t)(n32 + n64 + 2) * 16;
@@ -183,13 +189,14 @@ __host__ __device__ inline size_t stage_tab_offset(size_t tab_floats) { return (
 
 template <int NL>
 struct InfoStage {
-  static constexpr int N64 = NL + 5;
+  static constexpr int N64 = 2 * NL + 5;
   double* d;       // [N64][64]
   float* f;        // [n32][64]
   uint8_t* b;      // [2][64]
   uint64_t* tab;   // [slot][2]: base, stride (bytes)
   int lane, n32, nval, n4;
   bool any;        // some info array is written
+  bool defer;      // SimpleReacher observation trigonometry left to k_info_obs (o.qlog)
 
   // region: the block's staging area (after the basis table); e: the lane's env (< N)
   __device__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan_rows) {
@@ -205,6 +212,7 @@ struct InfoStage {
     n4 = (int)(N & 3);
     any = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector ||
           o.reward_dist;
+    defer = o.qlog != nullptr;
     const int ns = n32 + N64 + 2;
     // (lanes nval..63 of a partial last wave have left the kernel: the active lanes 0..nval-1 fill
     // every entry)
@@ -217,7 +225,9 @@ struct InfoStage {
           if (a && plan_rows) base = (const char*)(a + (s % NL) * N + e0);
           ks = (uint64_t)NL * N * 4;
         } else {
-          if (o.step_obs) base = (const char*)(o.step_obs + (s - 2 * NL) * N + e0);
+          const int p = s - 2 * NL;   // observation component (emit_obs order)
+          const bool later = defer && (p < 2 * NL || p == 3 * NL || p == 3 * NL + 1);
+          if (o.step_obs && !later) base = (const char*)(o.step_obs + p * N + e0);
           ks = (uint64_t)c.full_dim * N * 4;
         }
       } else if (s < n32 + N64) {
@@ -231,10 +241,13 @@ struct InfoStage {
         } else if (t <= NL + 2) {
           if (o.end_effector) base = (const char*)(o.end_effector + (t - NL - 1) * N + e0);
           ks = (uint64_t)2 * N * 8;
-        } else {
+        } else if (t < NL + 5) {
           const double* a = (t == NL + 3) ? o.reward_dist : o.reward_ctrl;
           if (a) base = (const char*)(a + e0);
           ks = (uint64_t)N * 8;
+        } else {
+          if (o.qlog) base = (const char*)(o.qlog + (t - NL - 5) * N + e0);
+          ks = (uint64_t)NL * N * 8;
         }
       } else {
         const uint8_t* a = (s == n32 + N64) ? o.is_collided : o.is_success;
@@ -255,6 +268,7 @@ struct InfoStage {
   __device__ __forceinline__ void ee(double x, double y) { d[(NL + 1) * 64 + lane] = x; d[(NL + 2) * 64 + lane] = y; }
   __device__ __forceinline__ void rdc(double x, double y) { d[(NL + 3) * 64 + lane] = x; d[(NL + 4) * 64 + lane] = y; }
   __device__ __forceinline__ void flags(uint8_t x, uint8_t y) { b[lane] = x; b[64 + lane] = y; }
+  __device__ __forceinline__ void ql(int dd, double x) { d[(NL + 5 + dd) * 64 + lane] = x; }
 
   // write the staged rows of sample kk (wave-uniform); every lane of the wave's envs active.  A full
   // wave (64 envs, 16-B aligned rows: N % 4 == 0) stores transposed 16-B pieces; otherwise (the

@@ -184,6 +184,10 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     }
   }
   if (log) {
+    if (ENV == ENV_SIMPLE && o.step_obs && !o.qlog) {
+      err = "SimpleReacher per-step observations need the qlog scratch (fgx_step attaches it)";
+      return -1;
+    }
     // + the four waves' info staging regions (InfoStage, fgx_device.h)
     const size_t ll = stage_tab_offset(lds / sizeof(float)) + (threads / 64) * stage_wave_bytes(NL, c.full_dim);
     if (ll > 64 * 1024 &&
@@ -194,6 +198,13 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     }
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, true>), dim3(blocks), dim3(threads), ll, stream, c, s,
                        params, dpos, dvel, o);
+    if constexpr (ENV == ENV_SIMPLE) {
+      if (o.qlog && o.step_obs) {   // the observation trigonometry of the logged rows (k_info_obs)
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) { err = std::string("k_episode launch: ") + hipGetErrorString(e); return -2; }
+        hipLaunchKernelGGL((k_info_obs<NL>), dim3(blocks, c.T), dim3(threads), 0, stream, c, o);
+      }
+    }
   }
   else
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, false>), dim3(blocks), dim3(threads), lds, stream, c, s,

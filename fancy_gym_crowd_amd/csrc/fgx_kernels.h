@@ -939,8 +939,20 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
 #pragma unroll
         for (int d = 0; d < NL; ++d) { ist.pos(d, pos[d]); ist.vel(d, vel[d]); }
       ist.rew(r.reward);
-      // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
-      if (o.step_obs) emit_obs(c, v, false, ist.obs_row(), nullptr, false, true, nullptr, nullptr, 64);
+      if constexpr (ENV == ENV_SIMPLE) {   // (the host always passes o.qlog with step_obs here)
+        // SimpleReacher: q for k_info_obs (cos / sin of q, FK's end effector - goal); here the
+        // components emit_obs computes without trigonometry, in its order
+#pragma unroll
+        for (int d = 0; d < NL; ++d) ist.ql(d, v.q[d]);
+        float* so = ist.obs_row();
+#pragma unroll
+        for (int d = 0; d < NL; ++d) so[(2 * NL + d) * 64] = (float)v.qd[d];
+        so[(3 * NL + 2) * 64] = (float)v.steps;
+        if (c.time_aware) so[(3 * NL + 3) * 64] = (float)((double)v.steps / (double)c.max_steps);
+      } else if (o.step_obs) {
+        // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
+        emit_obs(c, v, false, ist.obs_row(), nullptr, false, true, nullptr, nullptr, 64);
+      }
       if (ENV != ENV_SIMPLE) {
         ist.flags((uint8_t)r.coll, (uint8_t)r.success);
         ist.ee(v.jx[NL], v.jy[NL]);
@@ -1196,7 +1208,9 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
       const bool act = !stop && k < Te;
       if (__ballot(act) == 0) break;
       if (act) {
-        stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, true);
+        // (defer: FK only where the reward or the replanning schedule reads it, as without LOG)
+        stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{},
+                      ENV == ENV_SIMPLE ? (bool)c.sched_state : true);
       } else {
         L = min(L, k);
         if (k < c.T) pad_row(k, tg);
@@ -1212,6 +1226,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
       invalid_transition(c, s, o, e, v);
       return;
     }
+    if (ENV == ENV_SIMPLE && o.gsave) { o.gsave[e] = v.gx; o.gsave[N + e] = v.gy; }   // the episode's goal, for k_info_obs
   } else {
     while (!stop && k < Te) {
       stop = sample(k, std::integral_constant<int, -1>{}, std::integral_constant<int, 0>{}, c.sched_state);
@@ -1222,7 +1237,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   FGX_STAMP(o, e, 3);
   // the epilogue needs FK of the final q; a last sample at env step >= 199 (always a generic one)
   // has just computed it for its reward
-  if (ENV == ENV_SIMPLE && !LOG && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();
+  if (ENV == ENV_SIMPLE && !(v.steps - 1 >= 199 && !c.sched_state)) v.fk();
   const double ret = (L > 128 && rew_row) ? pairwise_strided(rew_row, N, L) : ps.result(L, split);
   FGX_STAMP(o, e, 4);
   if constexpr (PAIR) {   // the env's length once: from its even lane
@@ -1268,6 +1283,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     DevCfg c, DevState s, const float* __restrict__ params, const float* __restrict__ dpos,
     const float* __restrict__ dvel, Outputs o) {
   episode_body<ENV, MP, CTRL, NL, NB, LOG>(c, s, params, dpos, dvel, o);
+}
+
+// info_level 2, SimpleReacher: the per-step observation components that need trigonometry -- cos /
+// sin of every q (emit_obs: q[0]'s from FK) and the end effector minus the goal -- for every (sample,
+// env), one thread each, from the q the logging k_episode logged after every sample and the
+// episode's goal; NaN after trajectory_length.  The same FK / sincos / conversions as emit_obs on the
+// same q: bit-identical to computing them in the sample loop, where they cost ~9 f64 sincos per
+// sample of a lone wave's instruction stream; here they run at full occupancy.
+template <int NL>
+__global__ __launch_bounds__(256) void k_info_obs(DevCfg c, Outputs o) {
+  const int64_t N = c.N;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = blockIdx.y;
+  if (e >= N) return;
+  float* row = o.step_obs + t * c.full_dim * N + e;   // observation component p at row[p * N]
+  if (t >= o.tlen[e]) {
+    const float fnan = __builtin_nanf("");
+#pragma unroll
+    for (int p = 0; p < 2 * NL; ++p) row[p * N] = fnan;
+    row[3 * NL * N] = fnan;
+    row[(3 * NL + 1) * N] = fnan;
+    return;
+  }
+  Env<NL> v;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) v.q[d] = o.qlog[(t * NL + d) * N + e];
+  v.fk();
+  row[0] = (float)v.c[0];
+  row[NL * N] = (float)v.s[0];
+#pragma unroll
+  for (int d = 1; d < NL; ++d) {
+    double sn, cs;
+    fgx_sincos(v.q[d], &sn, &cs);
+    row[d * N] = (float)cs;
+    row[(NL + d) * N] = (float)sn;
+  }
+  row[3 * NL * N] = (float)(v.jx[NL] - o.gsave[e]);
+  row[(3 * NL + 1) * N] = (float)(v.jy[NL] - o.gsave[N + e]);
 }
 
 // ============================================================================ trajectories

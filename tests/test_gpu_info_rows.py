@@ -66,3 +66,33 @@ def test_info_rows_vs_oracle(ci, N):
                                                                                          "reward_ctrl")
         for name in keys:
             _rows(info, r_info, L, name, T)
+
+
+REPLAN = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
+
+
+@pytest.mark.parametrize("env_id,over", [("fancy_ProMP/LongSimpleReacher-v0", None),
+                                         ("fancy_ProDMP/SimpleReacher-v0", REPLAN),
+                                         ("fancy_ProDMP/HoleReacher-v0", None)])
+def test_logging_step_equals_fast_step(env_id, over):
+    """info_level=2 (the logging k_episode, + k_info_obs for SimpleReacher) and info_level=0 (the fast
+    kernels) give bit-identical steps; the last logged observation row of an env is its final
+    observation bit for bit (full observations: the replanning config has no context mask)."""
+    N = 1061
+    a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
+    b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    np.testing.assert_array_equal(np_(a.reset(seed=21)[0]), np_(b.reset(seed=21)[0]))
+    rng = np.random.default_rng(5)
+    full = a._eng.cfg.return_context == 0
+    for _ in range(3):
+        p = torch.from_numpy(rng.standard_normal((N, a.n_params), dtype=np.float32)).to(DEV)
+        oa, ra, ta, ua, ia = a.step(p)
+        ob, rb, tb, ub, ib = b.step(p)
+        for x, y in ((oa, ob), (ra, rb), (ta, tb), (ua, ub), (ia["trajectory_length"], ib["trajectory_length"]),
+                     (ia["final_observation"], ib["final_observation"])):
+            np.testing.assert_array_equal(np_(x), np_(y))
+        if full:
+            L = np_(ia["trajectory_length"]).astype(np.int64)
+            so = np_(ia["step_observations"])
+            last = so[np.arange(N), L - 1]
+            np.testing.assert_array_equal(last, np_(ia["final_observation"]))

@@ -40,7 +40,7 @@ PARTS = ("fetch", "write", "issue", "busy", "mix", "mfma", "stall")
 
 def kernel_family(name):
     """'fgx::k_episode_jp<1, 5, 5>(...)' -> 'k_episode_jp' (the name env.episode_kernel() reports)."""
-    m = re.search(r"(k_episode(?:_jp|_ws|_jl|_w2|_pair)?|k_traj_mfma)\b", name)
+    m = re.search(r"(k_episode(?:_jp|_ws|_jl|_w2|_pair)?|k_traj_mfma|k_info_obs)\b", name)
     return m.group(1) if m else None
 
 
@@ -52,7 +52,7 @@ def per_dispatch(src, want=None):
         agg, dur = collections.defaultdict(float), {}
         for r in csv.DictReader(open(path)):
             f = kernel_family(r["Kernel_Name"])
-            if f is None or (want is not None and f != want) or (want is None and f == "k_traj_mfma") or \
+            if f is None or (want is not None and f != want) or (want is None and f in ("k_traj_mfma", "k_info_obs")) or \
                     (fam is not None and f != fam):
                 continue
             fam, full = f, r["Kernel_Name"]
@@ -156,6 +156,12 @@ def main():
                 if "traffic_bytes_per_launch" in e and "bench_kernels_write" in e:
                     e["info_bytes_per_launch"] = e["bench_kernels_write"]["info_bytes"]
             entries.append(e)
+            if os.path.basename(d).endswith("log"):   # SimpleReacher: the observation kernel of the step
+                eo = entry(d, envs, workload, bid, a.round, want="k_info_obs")
+                if eo is not None:
+                    eo["kernel"] += "+info_level2"
+                    eo["info_level"] = 2
+                    entries.append(eo)
     out = {"method": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc_r03.sh); median over "
                      "dispatches of the per-dispatch sum over instances; traffic = (2*FETCH_SIZE + "
                      "WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count); valu_mix from the mix pass",
