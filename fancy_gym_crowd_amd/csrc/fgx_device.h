@@ -169,23 +169,32 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // ------------------------------------------------------------------ wave write-combining of info rows
 // The logging k_episode writes the verbose-2 per-step arrays ([T, N] / [T, X, N], up to GBs per BB
-// step).  One dword store per lane and row puts 256 B (f32) in flight per wave instruction; a lone
-// wave per SIMD then holds too few bytes in flight against the write latency of a GB-sized stream.
-// InfoStage collects the wave's values of one sample (every row of every array) in the wave's LDS
-// region, one slot of 64 lanes per row, and writes them back transposed: each lane stores 16
-// contiguous bytes (4 f32 / 2 f64 / 4 u8 envs), so one store instruction covers 4 f32 rows (or 2
-// f64 rows) of 64 envs = 1 KiB.  Slots: f32 [positions NL | velocities NL | step_obs full_dim],
+// step).  InfoStage collects the wave's values of one sample (every row of every array) in the wave's
+// LDS region, one slot of 64 lanes per row, and writes them back transposed: each lane stores 16
+// contiguous bytes (4 f32 / 2 f64 envs), so one store instruction covers 4 f32 rows (or 2 f64 rows)
+// of the wave's 64 envs = 1 KiB.  Slots: f32 [positions NL | velocities NL | step_obs full_dim],
 // f64 [step_actions NL | step_rewards | end_effector x, y | reward_dist | reward_ctrl | q NL (qlog)],
-// u8 [is_collided | is_success].  With qlog (defer) the step_obs slots k_info_obs writes (cos / sin
-// of q, end effector - goal) have no row here.  Per slot the table holds the address of the wave's first env in the
-// row of sample 0 and the row stride per sample (bytes).
+// u8 [is_collided | is_success].  Each array's row block of the sample is a wave-uniform (SGPR)
+// address and a lane's piece a 32-bit offset in it (global_store saddr form; fgx_step rejects
+// per-step arrays for N >= 2^24).  With qlog (defer) the step_obs components k_info_obs writes (cos /
+// sin of q, end effector - goal) are not stored here.
 __host__ __device__ inline int stage_n32(int nl, int full_dim) { return 2 * nl + full_dim; }
 __host__ __device__ inline int stage_n64(int nl) { return 2 * nl + 5; }
 __host__ __device__ inline size_t stage_wave_bytes(int nl, int full_dim) {
-  const int n32 = stage_n32(nl, full_dim), n64 = stage_n64(nl);
-  return (size_t)n64 * 512 + (size_t)n32 * 256 + 128 + (size_t)(n32 + n64 + 2) * 16;
+  return (size_t)stage_n64(nl) * 512 + (size_t)stage_n32(nl, full_dim) * 256 + 128;
 }
 __host__ __device__ inline size_t stage_tab_offset(size_t tab_floats) { return (tab_floats * 4 + 15) & ~(size_t)15; }
+
+// a wave-uniform global address as SGPRs, typed in the global address space: a generic pointer
+// rebuilt from integers would make every store through it a FLAT store, which also counts in
+// lgkmcnt, so that the next LDS wait of the wave would wait for the global stores as well
+typedef __attribute__((address_space(1))) char gchar;
+template <typename T>
+__device__ __forceinline__ gchar* uniform_ptr(T* p) {
+  const uint64_t a = (uint64_t)p;
+  return (gchar*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32) |
+                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+}
 
 template <int NL>
 struct InfoStage {
@@ -193,71 +202,30 @@ struct InfoStage {
   double* d;       // [N64][64]
   float* f;        // [n32][64]
   uint8_t* b;      // [2][64]
-  uint64_t* tab;   // [slot][2]: base, stride (bytes)
-  int lane, n32, nval, n4;
+  int64_t N, e0;
+  int lane, n32, nval, full_dim;
   bool any;        // some info array is written
+  bool full;       // 64 envs, rows 16-B aligned (N % 4 == 0): transposed 16-B pieces
   bool defer;      // SimpleReacher observation trigonometry left to k_info_obs (o.qlog)
+  bool plan_rows;  // positions / velocities are this kernel's (not a given plan)
 
   // region: the block's staging area (after the basis table); e: the lane's env (< N)
-  __device__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan_rows) {
+  __device__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan) {
     lane = (int)(threadIdx.x & 63);
+    full_dim = c.full_dim;
     n32 = stage_n32(NL, c.full_dim);
     char* w = region + (size_t)(threadIdx.x >> 6) * stage_wave_bytes(NL, c.full_dim);
     d = (double*)w;
     f = (float*)(w + N64 * 512);
     b = (uint8_t*)(w + N64 * 512 + n32 * 256);
-    tab = (uint64_t*)(w + N64 * 512 + n32 * 256 + 128);
-    const int64_t N = c.N, e0 = e - lane;
+    N = c.N;
+    e0 = e - lane;
     nval = (int)min((int64_t)64, N - e0);
-    n4 = (int)(N & 3);
+    full = nval == 64 && (N & 3) == 0;
     any = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector ||
           o.reward_dist;
     defer = o.qlog != nullptr;
-    const int ns = n32 + N64 + 2;
-    // (lanes nval..63 of a partial last wave have left the kernel: the active lanes 0..nval-1 fill
-    // every entry)
-    for (int s = lane; s < ns; s += nval) {
-      const char* base = nullptr;
-      uint64_t ks = 0;
-      if (s < n32) {
-        if (s < 2 * NL) {
-          const float* a = (s < NL) ? o.positions : o.velocities;
-          if (a && plan_rows) base = (const char*)(a + (s % NL) * N + e0);
-          ks = (uint64_t)NL * N * 4;
-        } else {
-          const int p = s - 2 * NL;   // observation component (emit_obs order)
-          const bool later = defer && (p < 2 * NL || p == 3 * NL || p == 3 * NL + 1);
-          if (o.step_obs && !later) base = (const char*)(o.step_obs + p * N + e0);
-          ks = (uint64_t)c.full_dim * N * 4;
-        }
-      } else if (s < n32 + N64) {
-        const int t = s - n32;
-        if (t < NL) {
-          if (o.step_actions) base = (const char*)(o.step_actions + t * N + e0);
-          ks = (uint64_t)NL * N * 8;
-        } else if (t == NL) {
-          if (o.step_rewards) base = (const char*)(o.step_rewards + e0);
-          ks = (uint64_t)N * 8;
-        } else if (t <= NL + 2) {
-          if (o.end_effector) base = (const char*)(o.end_effector + (t - NL - 1) * N + e0);
-          ks = (uint64_t)2 * N * 8;
-        } else if (t < NL + 5) {
-          const double* a = (t == NL + 3) ? o.reward_dist : o.reward_ctrl;
-          if (a) base = (const char*)(a + e0);
-          ks = (uint64_t)N * 8;
-        } else {
-          if (o.qlog) base = (const char*)(o.qlog + (t - NL - 5) * N + e0);
-          ks = (uint64_t)NL * N * 8;
-        }
-      } else {
-        const uint8_t* a = (s == n32 + N64) ? o.is_collided : o.is_success;
-        if (a) base = (const char*)(a + e0);
-        ks = (uint64_t)N;
-      }
-      tab[2 * s] = (uint64_t)base;
-      tab[2 * s + 1] = ks;
-    }
-    wave_lds_sync();
+    plan_rows = plan;
   }
   // the lane's value of slot s of the current sample
   __device__ __forceinline__ void pos(int dd, float x) { f[dd * 64 + lane] = x; }
@@ -270,57 +238,71 @@ struct InfoStage {
   __device__ __forceinline__ void flags(uint8_t x, uint8_t y) { b[lane] = x; b[64 + lane] = y; }
   __device__ __forceinline__ void ql(int dd, double x) { d[(NL + 5 + dd) * 64 + lane] = x; }
 
-  // write the staged rows of sample kk (wave-uniform); every lane of the wave's envs active.  A full
-  // wave (64 envs, 16-B aligned rows: N % 4 == 0) stores transposed 16-B pieces; otherwise (the
-  // partial last wave, whose lanes past N have left the kernel, or N % 4 != 0) every lane stores its
-  // own element of each row.
-  __device__ void flush(int kk) {
+  // components c0..X-1 (at most MAXX) of sample k of the [T, X, N] array A from the staging slots
+  // st[comp * 64 ..]; skip(comp): not this kernel's
+  template <typename T, int MAXX, typename Skip>
+  __device__ __forceinline__ void rows(T* A, int X, int c0, const T* st, uint32_t k, Skip skip) const {
+    constexpr int PER = 16 / (int)sizeof(T);   // envs per lane piece
+    constexpr int LPR = 64 / PER;              // lanes per row piece
+    constexpr int RPI = 64 / LPR;              // rows per store instruction
+    gchar* rb = uniform_ptr(A + (uint64_t)k * (uint64_t)X * (uint64_t)N);   // the sample's row block
+    if (full) {
+      typedef T V __attribute__((ext_vector_type(PER)));
+      const int q = lane % LPR, r = lane / LPR;
+#pragma unroll
+      for (int c = 0; c < MAXX; c += RPI) {
+        if (c + c0 >= X) break;
+        const int comp = c0 + c + r;
+        const V x = *(const V*)(st + comp * 64 + PER * q);
+        if (comp < X && !skip(comp))
+          *(__attribute__((address_space(1))) V*)(rb + (uint32_t)(((uint32_t)comp * (uint32_t)N +
+                                                                   (uint32_t)(e0 + PER * q)) * sizeof(T))) = x;
+      }
+    } else {   // partial last wave (its lanes past N have left the kernel) or N % 4 != 0: own element
+      for (int comp = c0; comp < X; ++comp)
+        if (!skip(comp))
+          *(__attribute__((address_space(1))) T*)(rb + (uint32_t)(((uint32_t)comp * (uint32_t)N +
+                                                                   (uint32_t)(e0 + lane)) * sizeof(T))) =
+              st[comp * 64 + lane];
+    }
+  }
+
+  // write the staged rows of sample kk (wave-uniform); every lane of the wave's envs active
+  __device__ void flush(int kk, const Outputs& o) {
     if (!any) return;
     wave_lds_sync();
     const uint32_t k = (uint32_t)kk;
-    if (nval == 64 && n4 == 0) {
-      {   // f32: 4 slots per instruction, lane = (slot within the group, 4-env quad)
-        const int q = lane & 15;
-        for (int g = 0; g < n32; g += 4) {
-          const int s = g + (lane >> 4);
-          if (s >= n32) continue;
-          const uint64_t base = tab[2 * s];
-          if (!base) continue;
-          const float4 x = *(const float4*)(f + s * 64 + 4 * q);
-          *(float4*)((float*)(base + (uint64_t)k * (uint32_t)tab[2 * s + 1]) + 4 * q) = x;
-        }
-      }
-      {   // f64: 2 slots per instruction, lane = (slot within the group, env pair)
-        const int q = lane & 31;
-        for (int g = 0; g < N64; g += 2) {
-          const int s = g + (lane >> 5);
-          if (s >= N64) continue;
-          const uint64_t base = tab[2 * (n32 + s)];
-          if (!base) continue;
-          const double2 x = *(const double2*)(d + s * 64 + 2 * q);
-          *(double2*)((double*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + s) + 1]) + 2 * q) = x;
-        }
-      }
-      if (lane < 32) {   // u8: lanes 0-15 is_collided, 16-31 is_success, 4 envs each
-        const int s = lane >> 4, q = lane & 15;
-        const uint64_t base = tab[2 * (n32 + N64 + s)];
-        if (base) {
-          const uint32_t x = *(const uint32_t*)(b + s * 64 + 4 * q);
-          *(uint32_t*)((uint8_t*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + N64 + s) + 1]) + 4 * q) = x;
-        }
-      }
-    } else {
-      for (int s = 0; s < n32; ++s) {
-        const uint64_t base = tab[2 * s];
-        if (base) ((float*)(base + (uint64_t)k * (uint32_t)tab[2 * s + 1]))[lane] = f[s * 64 + lane];
-      }
-      for (int s = 0; s < N64; ++s) {
-        const uint64_t base = tab[2 * (n32 + s)];
-        if (base) ((double*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + s) + 1]))[lane] = d[s * 64 + lane];
-      }
-      for (int s = 0; s < 2; ++s) {
-        const uint64_t base = tab[2 * (n32 + N64 + s)];
-        if (base) ((uint8_t*)(base + (uint64_t)k * (uint32_t)tab[2 * (n32 + N64 + s) + 1]))[lane] = b[s * 64 + lane];
+    auto none = [](int) { return false; };
+    if (o.positions && plan_rows) {
+      rows<float, NL>(o.positions, NL, 0, f, k, none);
+      rows<float, NL>(o.velocities, NL, 0, f + NL * 64, k, none);
+    }
+    if (o.step_obs) {
+      const float* so = f + 2 * NL * 64;
+      if (defer)   // qd, steps, time: components 2 NL .. (cos / sin of q and the end effector: k_info_obs)
+        rows<float, kMaxObs + 1 - (2 * NL & ~3)>(o.step_obs, full_dim, 2 * NL & ~3, so, k,
+                                                 [](int p) { return p < 2 * NL || p == 3 * NL || p == 3 * NL + 1; });
+      else
+        rows<float, kMaxObs + 1>(o.step_obs, full_dim, 0, so, k, none);
+    }
+    if (o.step_actions) rows<double, NL>(o.step_actions, NL, 0, d, k, none);
+    if (o.step_rewards) rows<double, 1>(o.step_rewards, 1, 0, d + NL * 64, k, none);
+    if (o.end_effector) rows<double, 2>(o.end_effector, 2, 0, d + (NL + 1) * 64, k, none);
+    if (o.reward_dist) {
+      rows<double, 1>(o.reward_dist, 1, 0, d + (NL + 3) * 64, k, none);
+      rows<double, 1>(o.reward_ctrl, 1, 0, d + (NL + 4) * 64, k, none);
+    }
+    if (o.qlog) rows<double, NL>(o.qlog, NL, 0, d + (NL + 5) * 64, k, none);
+    if (o.is_collided) {   // [T, N] u8 rows: lanes 0-15 is_collided, 16-31 is_success, 4 envs each
+      gchar* rc = uniform_ptr(o.is_collided + (uint64_t)k * (uint64_t)N);
+      gchar* rs = uniform_ptr(o.is_success + (uint64_t)k * (uint64_t)N);
+      typedef __attribute__((address_space(1))) uint32_t gu32;
+      if (full) {
+        if (lane < 16) *(gu32*)(rc + (uint32_t)(e0 + 4 * lane)) = *(const uint32_t*)(b + 4 * lane);
+        else if (lane < 32) *(gu32*)(rs + (uint32_t)(e0 + 4 * (lane - 16))) = *(const uint32_t*)(b + 64 + 4 * (lane - 16));
+      } else {
+        rc[(uint32_t)(e0 + lane)] = (char)b[lane];
+        rs[(uint32_t)(e0 + lane)] = (char)b[64 + lane];
       }
     }
     wave_lds_sync();

@@ -1215,12 +1215,12 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
         L = min(L, k);
         if (k < c.T) pad_row(k, tg);
       }
-      if (k < c.T) ist.flush(__builtin_amdgcn_readfirstlane(k));
+      if (k < c.T) ist.flush(__builtin_amdgcn_readfirstlane(k), o);
     }
     L = min(L, k);
     for (int kk = __builtin_amdgcn_readfirstlane(k); kk < c.T; ++kk) {
       pad_row(kk, tg);
-      ist.flush(kk);
+      ist.flush(kk, o);
     }
     if (invalid) {
       invalid_transition(c, s, o, e, v);
