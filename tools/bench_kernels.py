@@ -193,6 +193,25 @@ if __name__ == "__main__":
                                   info_bytes=ib, info_GBps_step_wall=ib / us / 1e3)), flush=True)
             del env
             torch.cuda.empty_cache()
+    if "levels" in which:   # the public step() at info_level 0 / 1 / 2 (what the logging kernel's stores cost)
+        for lvl in (0, 1, 2):
+            env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=65536, device=dev, info_level=lvl)
+            env.reset(seed=0)
+            params = torch.randn((65536, env.n_params), device=dev)
+            for _ in range(2):
+                env.step(params)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                env.step(params)
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps(dict(kernel="step(info_level=%d)" % lvl, config="fancy_ProMP/LongSimpleReacher-v0",
+                                  envs=65536, us_per_step=e0.elapsed_time(e1) / 5 * 1e3,
+                                  episode_kernel=env.episode_kernel())), flush=True)
+            del env
+            torch.cuda.empty_cache()
     if "scan" in which:   # metric env over the envs-per-GPU axis (occupancy / tail effects)
         for n in (4096, 8192, 16384, 32768, 49152, 65536, 81920, 98304, 131072, 262144):
             episode("fancy_ProMP/LongSimpleReacher-v0", n, label="scan: ProMP LongSimpleReacher", reps=10)
