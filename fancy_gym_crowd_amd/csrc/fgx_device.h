@@ -320,6 +320,23 @@ __device__ __forceinline__ int wave_max(int x) {
   for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, 64));
   return __builtin_amdgcn_readfirstlane(x);
 }
+// The same on the joint-lane kernels' prologue (all 64 lanes active there, lone waves at the shard
+// sizes): within each row of 16 lanes by DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror: VALU, no LDS round trip), then the four rows' values by readlane on the scalar unit;
+// __shfl_xor lowers to a chain of six ds_bpermute round trips, ~0.6 k cycles for a lone wave
+// (A/B, profiles/r03_shard_ab_s16.jsonl: jl 8192 envs 24.1 -> 23.8 us; k_episode keeps the shuffles,
+// whose one reduction measured 0.7% faster there).
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_dpp(int x, Op op) {
+  x = op(x, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));
+  x = op(x, __builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));
+  return op(op(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+            op(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+}
+__device__ __forceinline__ int wave_min_dpp(int x) { return wave_reduce_dpp(x, [](int a, int b) { return min(a, b); }); }
+__device__ __forceinline__ int wave_max_dpp(int x) { return wave_reduce_dpp(x, [](int a, int b) { return max(a, b); }); }
 // the partner lane's value in lane pairs (2i, 2i + 1): DPP quad_perm [1, 0, 3, 2]; both lanes of a
 // pair are always active together (k_episode_pair)
 __device__ __forceinline__ int pair_swap32(int x) { return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); }

@@ -84,10 +84,13 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   FGX_STAMP(o, wst, 6);
   FGX_STAMP(o, wst, 0);
 
+  // the joint's state first: its loads need nothing the segment computes (they are in flight while
+  // the segment's loads return and its wave reductions run)
+  double q = s.q[d * N + e], qd = s.qd[d * N + e];
   // ---- the env's segment; wave-uniform bounds over the valid lanes
   JpSeg sg;
   sg.init(c, s, e, valid);
-  const int Lmin = wave_min(valid ? sg.L : 0x7fffffff), Lmax = wave_max(valid ? sg.L : 0);
+  const int Lmin = wave_min_dpp(valid ? sg.L : 0x7fffffff), Lmax = wave_max_dpp(valid ? sg.L : 0);
   const int lead = vmask ? __builtin_ctzll(vmask) : 0;
   FGX_STAMP(o, wst, 12);
 
@@ -99,7 +102,6 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     dg = (j == d) ? c.dg[j] : dg;
   }
   const int nb = NB ? NB : c.nb;
-  double q = s.q[d * N + e], qd = s.qd[d * N + e];
   Traj<MP, 1, NB> tg;
   const int s0 = c.replan ? sg.steps : 0;   // init_time = current_traj_steps * dt when replanning
   auto init_traj = [&]() __attribute__((always_inline)) {

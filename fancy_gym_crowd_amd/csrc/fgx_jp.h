@@ -105,7 +105,7 @@ __global__ __launch_bounds__(NL * 64, 5) void k_episode_jp(DevCfg c, DevState s,
   // ---- the env's segment (every wave reads the same 64 envs: wave reductions agree across waves)
   JpSeg sg;
   sg.init(c, s, e, valid);
-  const int Lmin = wave_min(sg.L), Lmax = wave_max(sg.L);
+  const int Lmin = wave_min_dpp(sg.L), Lmax = wave_max_dpp(sg.L);
   const bool uni = Lmin == Lmax;   // one segment length (hence layout) for the wave: uniform phases
   const int hs_u = __builtin_amdgcn_readfirstlane(sg.hs), bend_u = __builtin_amdgcn_readfirstlane(sg.bend);
 
