@@ -284,27 +284,41 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
             ev0[k].record()
             env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
             ev1[k].record()
+    # the collective and the closing barrier are timed apart from the kernels (per rank), so that a
+    # multi-GPU point separates kernel time from collective latency
+    coll_ms = barrier_ms = 0.0
     if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
+        ec0, ec1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ec0.record()
         all_ret = shard.gather_returns(ret.to(coll_dev))
+        ec1.record()
     torch.cuda.synchronize()
     if dist is not None:
+        tb = time.perf_counter()
         dist.barrier()
+        barrier_ms = (time.perf_counter() - tb) * 1e3
+        coll_ms = ec0.elapsed_time(ec1)
     elapsed = time.perf_counter() - t0
     inner_local = int(acc.sum().item())
     if graph is not None:
         kern_ms = ev0[0].elapsed_time(ev1[0]) / K
     else:
         kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
+    timing_local = [kern_ms, coll_ms, barrier_ms, elapsed * 1e3]
     if dist is not None:
         elapsed = shard.max_over_ranks(elapsed, coll_dev)
         inner = shard.sum_over_ranks(inner_local, coll_dev)
         assert all_ret.numel() == N * world
         shards = shard.gather_ints([lo, lo + N, inner_local], coll_dev)
+        timing = shard.gather_floats(timing_local, coll_dev)
     else:
         inner = inner_local
         shards = [[lo, lo + N, inner_local]]
+        timing = [timing_local]
+    per_rank = [{"rank": i, "kernel_ms_per_step": t[0], "collective_ms": t[1], "barrier_ms": t[2], "wall_ms": t[3]}
+                for i, t in enumerate(timing)]
     return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
-                shards=shards,
+                shards=shards, per_rank=per_rank,
                 launch="hip graph of the K steps" if graph is not None else "eager")
 
 
@@ -378,6 +392,9 @@ def main():
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch the K steps eagerly instead of replaying them as one HIP graph")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group (and run the return gather) even for one rank: "
+                         "exercises the RCCL path on a one-GPU box (tests/test_gpu_rccl.py)")
     args = ap.parse_args()
 
     launched = "WORLD_SIZE" in os.environ
@@ -400,7 +417,7 @@ def main():
     rehearsal = world > 1 and torch.cuda.device_count() < world
     gpu = 0 if rehearsal else local
     coll_dev = "cpu" if rehearsal else torch.device("cuda", gpu)
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         if rehearsal:
@@ -454,6 +471,12 @@ def main():
                                                      else "")) if launched else "single process",
             # per rank: [first global env, end, inner env steps in the timed region]
             "shards": r["shards"],
+            # per rank: kernel time per BB step (HIP events), the return all_gather (events around it)
+            # and the closing barrier (host), all inside the timed region
+            "timing": {"kernel_ms_per_step_max": max(t["kernel_ms_per_step"] for t in r["per_rank"]),
+                       "collective_ms_max": max(t["collective_ms"] for t in r["per_rank"]),
+                       "barrier_ms_max": max(t["barrier_ms"] for t in r["per_rank"]),
+                       "per_rank": r["per_rank"]},
             "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds, lib_build_id()),
         }
         if weak is not None:

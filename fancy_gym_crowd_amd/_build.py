@@ -22,8 +22,10 @@ INC = os.path.join(HERE, "..", "include")
 LIB = os.path.join(HERE, "libfgx.so")
 STAMP = LIB + ".buildid"
 OBJDIR = os.path.join(HERE, "csrc", "build")
-SOURCES = ["fgx_ep_simple_gen.hip", "fgx_ep_hole_gen.hip", "fgx_ep_via_gen.hip", "fgx_ep_simple.hip",
-           "fgx_ep_hole.hip", "fgx_ep_via.hip", "fgx_ep_jl.hip", "fgx_api.hip"]
+# (the longest units first: the pool starts them before the short ones)
+SOURCES = ["fgx_ep_hole_gen.hip", "fgx_ep_hole.hip", "fgx_ep_simple_gen.hip", "fgx_ep_simple.hip",
+           "fgx_ep_via_gen.hip", "fgx_ep_via.hip", "fgx_ep_jl.hip"] + \
+          [f"fgx_ep_nl{n}.hip" for n in (1, 3, 4, 6, 7, 8)] + ["fgx_api.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # numerics: every expression rounds like the numpy reference; fmas only where written
          "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -149,7 +151,7 @@ def build_variant(out, defines=(), verbose=False):
         with open(obj + ".key", "w") as f:
             f.write(key)
         return obj
-    with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8)) as ex:
         objs = list(ex.map(one, SOURCES))
     subprocess.run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out], check=True)
     return out
@@ -160,7 +162,7 @@ def build(force=False, verbose=True):
     if not force and built_id() == bid:
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
-    with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 8)) as ex:
         objs = list(ex.map(lambda s: _compile(s, bid, verbose, force), SOURCES))   # force: no cached objects
     cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
     if verbose:

@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfgx.so")
 
-FGX_ABI_VERSION = 7
+FGX_ABI_VERSION = 8
 INNER_STEPS_LEN = 128 * 16   # include/fgx.h FGX_INNER_STEPS_LEN (partial counters, sum them)
 ENV_SIMPLE, ENV_HOLE, ENV_VIA = 0, 1, 2
 REW_SIMPLE, REW_VEL_ACC, REW_UNBOUNDED = 0, 1, 2
@@ -47,7 +47,8 @@ class FgxConfig(ctypes.Structure):
         (n, ctypes.c_int32) for n in ("valid_flags", "invalid_obs", "invalid_terminated", "invalid_truncated")] + [
         (n, ctypes.c_double) for n in ("invalid_reward", "valid_tau_lo", "valid_tau_hi", "valid_delay_lo",
                                        "valid_delay_hi")] + [
-        ("valid_pos_lo", ctypes.c_double * 8), ("valid_pos_hi", ctypes.c_double * 8)]
+        ("valid_pos_lo", ctypes.c_double * 8), ("valid_pos_hi", ctypes.c_double * 8),
+        ("basis_dt", ctypes.c_double)]
 
 
 class FgxDims(ctypes.Structure):
@@ -110,9 +111,7 @@ def load(path=None):
         fn.restype = res
         fn.argtypes = args
     abi = lib.fgx_abi_version()
-    # (FGX_LIB_ABI6=1: an experiment may load an ABI-6 build -- same config layout, single-counter
-    # inner_steps, which still sums right in the ABI-7 counter array)
-    if abi != FGX_ABI_VERSION and not (abi == 6 and os.environ.get("FGX_LIB") and os.environ.get("FGX_LIB_ABI6")):
+    if abi != FGX_ABI_VERSION:
         raise FgxError("libfgx ABI version mismatch")
     if path == LIB_PATH:   # build provenance: the in-tree library must match the in-tree sources
         from . import _build

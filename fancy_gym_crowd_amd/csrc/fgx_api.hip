@@ -12,7 +12,7 @@
 
 #include "../../include/fgx.h"
 #include "fgx_kernels.h"
-#include "fgx_tables.h"
+#include "fgx_tables_k.h"
 #include "fgx_aux.h"
 #include "fgx_dispatch.h"
 #include "fgx_learned.h"
@@ -65,8 +65,22 @@ size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 // (fgx_ep_<env>.hip, fgx_ep_<env>_gen.hip) so that the build compiles them in parallel.
 #define FGX_FOR_NL(X) X(2) X(5)
 
+// the kernel families of the other link counts (fgx_ep_nl.h); null for 2 and 5
+static const NlOps* nl_ops(int nl) {
+  switch (nl) {
+    case 1: return fgx_nl_ops_1();
+    case 3: return fgx_nl_ops_3();
+    case 4: return fgx_nl_ops_4();
+    case 6: return fgx_nl_ops_6();
+    case 7: return fgx_nl_ops_7();
+    case 8: return fgx_nl_ops_8();
+  }
+  return nullptr;
+}
+
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
+  if (const NlOps* ops = nl_ops(h.dc.nl)) return ops->episode(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
   const bool gen = mp != MP_GIVEN && h.dc.nb != 5;   // generic basis-count instantiations
   if (h.dc.env == ENV_SIMPLE)
     return (gen ? fgx_launch_episode_simple_gen : fgx_launch_episode_simple)(h.dc, h.st, mp, params, dpos, dvel, o,
@@ -90,7 +104,8 @@ static int launch_reset(const Handle& h, const uint64_t* seeds, const uint8_t* m
   }
   FGX_FOR_NL(X)
 #undef X
-  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+  if (const NlOps* ops = nl_ops(h.dc.nl)) return ops->reset(h.dc, h.st, seeds, mask, rs_mode, obs, stream, g_err);
+  return fail(FGX_E_UNSUPPORTED, "n_links must be in 1..8");
 }
 
 static int launch_traj_env(const Handle& h, const float* params, float* pos, float* vel, hipStream_t stream,
@@ -102,13 +117,15 @@ static int launch_traj_env(const Handle& h, const float* params, float* pos, flo
                      h.env_tab, pos, vel, h.plan_len, info_pos, info_vel)
 #define LAUNCH(MPV, NLV) do { if (h.dc.nb == 5) LAUNCH1(MPV, NLV, 5); else LAUNCH1(MPV, NLV, 0); } while (0)
   const int mp = h.dc.mp, nl = h.dc.nl;
+  if (const NlOps* ops = nl_ops(nl))
+    return ops->traj_env(h.dc, h.st, params, h.env_tab, pos, vel, h.plan_len, info_pos, info_vel, stream, g_err);
   if (mp == MP_PROMP && nl == 2) LAUNCH(MP_PROMP, 2);
   else if (mp == MP_PROMP && nl == 5) LAUNCH(MP_PROMP, 5);
   else if (mp == MP_DMP && nl == 2) LAUNCH(MP_DMP, 2);
   else if (mp == MP_DMP && nl == 5) LAUNCH(MP_DMP, 5);
   else if (mp == MP_PRODMP && nl == 2) LAUNCH(MP_PRODMP, 2);
   else if (mp == MP_PRODMP && nl == 5) LAUNCH(MP_PRODMP, 5);
-  else return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+  else return fail(FGX_E_UNSUPPORTED, "n_links must be in 1..8");
 #undef LAUNCH1
 #undef LAUNCH
   HIP_TRY(hipGetLastError());
@@ -158,8 +175,13 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
     if (c.mp_kind == FGX_MP_PRODMP && c.phase_kind != FGX_PHASE_EXP)
       return fail(FGX_E_INVALID, "prodmp needs the exp phase generator");   // basis_generator_factory.py:14
     if (!(c.tau > 0.0) || !(c.dt > 0.0) || !std::isfinite(c.tau)) return fail(FGX_E_INVALID, "tau/dt must be positive");
-    // a negative delay would look up basis rows after the current one (prodmp_delay_index)
-    if (!(c.delay >= 0.0) || !std::isfinite(c.delay)) return fail(FGX_E_INVALID, "delay must be finite and >= 0");
+    if (!std::isfinite(c.delay)) return fail(FGX_E_INVALID, "delay must be finite");
+    // ProDMP: a negative delay would look up basis rows after the current one (prodmp_delay_index);
+    // ProMP / DMP clip the phase max((t - delay) / tau, 0) and take any delay, as the reference does
+    if (c.mp_kind == FGX_MP_PRODMP && !(c.delay >= 0.0)) return fail(FGX_E_INVALID, "ProDMP delay must be >= 0");
+    if (!(c.basis_dt >= 0.0) || !std::isfinite(c.basis_dt)) return fail(FGX_E_INVALID, "basis_dt must be finite and >= 0");
+    if (c.basis_dt > 0.0 && c.basis_dt != c.dt && c.mp_kind != FGX_MP_PRODMP)
+      return fail(FGX_E_INVALID, "basis_dt is a ProDMP basis generator option");
   }
   if (c.time_aware && c.return_context) return fail(FGX_E_INVALID, "time_aware with context observation");
   std::memset(&d, 0, sizeof(d));
@@ -259,6 +281,9 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.delay = c.delay;
   d.alpha_phase = c.alpha_phase;
   d.bandwidth = c.bandwidth;
+  d.bdt = c.basis_dt > 0.0 ? c.basis_dt : c.dt;
+  if (c.mp_kind == FGX_MP_PRODMP && prodmp_fine_rows(d.dt, d.bdt, d.rows, d.tau, d.delay) > (1 << 20))
+    return fail(FGX_E_UNSUPPORTED, "ProDMP precompute grid too fine (basis dt far below the env dt)");
   if (c.n_gains != 0 && c.n_gains != c.n_links)   // p_gains * (des_pos - c_pos) must broadcast
     return fail(FGX_E_INVALID, "per-joint PD gains must have n_links entries");
   for (int k = 0; k < kMaxLinks; ++k) {
@@ -408,10 +433,11 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
     hipLaunchKernelGGL(k_tables_rbf, dim3(blk), dim3(thr), 0, 0, d, cfg->tau, cfg->delay, cfg->alpha_phase,
                        cfg->bandwidth, h->tables);
   } else if (d.mp == MP_PRODMP) {
-    e = hipMalloc(&h->scratch, sizeof(double) * d.rows * 2 * d.nb + 64);
+    const int Rf = prodmp_fine_rows(d.dt, d.bdt, d.rows, cfg->tau, cfg->delay);   // fine-grid rows
+    e = hipMalloc(&h->scratch, sizeof(double) * (size_t)Rf * 2 * d.nb + 64);
     if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_NOMEM, "hipMalloc scratch"); }
     hipLaunchKernelGGL(k_tables_prodmp, dim3(1), dim3(256), 0, 0, d, cfg->tau, cfg->delay, cfg->alpha_phase,
-                       cfg->bandwidth, h->scratch, h->tables);
+                       cfg->bandwidth, Rf, h->scratch, h->tables);
   }
   if (d.mp != MP_NONE && d.rows > 0) {
     const int n = tables_t_rows(d.rows) * d.stride;
@@ -618,6 +644,7 @@ int fgx_trajectory(void* handle, const float* params, float* des_pos, float* des
   if (!h) return fail(FGX_E_INVALID, "null handle");
   if (!params || !des_pos || !des_vel) return fail(FGX_E_INVALID, "null argument");
   if (h->learned()) return launch_traj_env(*h, params, des_pos, des_vel, (hipStream_t)stream);
+  if (const NlOps* ops = nl_ops(h->dc.nl)) return ops->traj(h->dc, h->st, params, des_pos, des_vel, (hipStream_t)stream, g_err);
   return launch_trajectory(h->dc, h->st, params, des_pos, des_vel, (hipStream_t)stream, g_err);
 }
 
@@ -649,7 +676,9 @@ int fgx_step_raw(void* handle, const float* actions, float* obs, double* reward,
   }
   FGX_FOR_NL(X)
 #undef X
-  return fail(FGX_E_UNSUPPORTED, "n_links not instantiated (supported: 2, 5)");
+  if (const NlOps* ops = nl_ops(h->dc.nl))
+    return ops->step_raw(h->dc, h->st, actions, obs, reward, terminated, truncated, final_obs, autoreset, lds, s, g_err);
+  return fail(FGX_E_UNSUPPORTED, "n_links must be in 1..8");
 }
 
 int fgx_get_state(void* handle, double* q, double* qd, double* goal, double* hole, int32_t* steps, void* stream) {

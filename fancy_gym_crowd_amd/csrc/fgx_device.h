@@ -62,6 +62,7 @@ struct DevCfg {
   double hole_w0, hole_d0, hole_x0, penalty, weights_scale, goal_scale, alpha;
   double via_x0, via_y0, tgt_x0, tgt_y0;
   double delay, alpha_phase, bandwidth;   // phase / basis generator (per-env tables)
+  double bdt;                             // ProDMP basis generator dt (its precompute grid; = dt by default)
   float tau_lo32, tau_hi32, delay_lo32, delay_hi32;   // action-space bounds of tau / delay
   float ws32, gs32, alpha32, beta32;
   // trajectory validity (include/fgx.h FGX_VALID_*; only the logging k_episode reads these)
@@ -398,6 +399,23 @@ __device__ __forceinline__ double div_rcp64(double x, double d, double r) {
   const double q = x * r;
   const double e = __builtin_fma(-q, d, x);
   return __builtin_fma(e, r, q);
+}
+
+// np.sum of NL values v(0), ..., v(NL - 1) in numpy's pairwise_sum order (umath loops_utils.h):
+// a left-to-right loop for NL < 8 (its leading 0 + v(0) is v(0) for the engine's summands, squares
+// that are never -0), for NL = 8 eight accumulators combined as ((r0 + r1) + (r2 + r3)) +
+// ((r4 + r5) + (r6 + r7)).  add: the two-operand add (fadd for the f64 issue-rate form).
+template <int NL, typename T, typename V, typename Add>
+__device__ __forceinline__ T np_sum(V v, Add add) {
+  static_assert(NL >= 1 && NL <= 8, "n_links in 1..8");
+  if constexpr (NL < 8) {
+    T s = v(0);
+#pragma unroll
+    for (int d = 1; d < NL; ++d) s = add(s, v(d));
+    return s;
+  } else {
+    return add(add(add(v(0), v(1)), add(v(2), v(3))), add(add(v(4), v(5)), add(v(6), v(7))));
+  }
 }
 
 // np.linalg.norm of a 2-vector == sqrt(ddot) == sqrt(fma(y, y, x*x)) (OpenBLAS order)

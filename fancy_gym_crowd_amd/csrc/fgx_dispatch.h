@@ -24,6 +24,31 @@ int fgx_launch_episode_jl(const fgx::DevCfg& c, const fgx::DevState& s, int mp, 
                           const fgx::Outputs& o, hipStream_t stream, std::string& err);
 
 namespace fgx {
+// Link counts other than the registered 2 and 5 (include/fgx.h: n_links 1..8; base_reacher.py:17-39
+// takes any count and bb_env_constructor forwards env kwargs, envs/registry.py:280-281): one
+// translation unit per count (fgx_ep_nl<n>.hip -> fgx_ep_nl.h) with the logging k_episode for every
+// env kind / MP kind / controller plus the reset, step-based, trajectory and learned-phase kernels.
+struct NlOps {
+  int (*episode)(const DevCfg& c, const DevState& s, int mp, const float* params, const float* dpos, const float* dvel,
+                 const Outputs& o, hipStream_t stream, std::string& err);
+  int (*reset)(const DevCfg& c, const DevState& s, const uint64_t* seeds, const uint8_t* mask, int rs_mode, float* obs,
+               hipStream_t stream, std::string& err);
+  int (*step_raw)(const DevCfg& c, const DevState& s, const float* act, float* obs, double* rew, uint8_t* term,
+                  uint8_t* trunc, float* final_obs, int autoreset, size_t lds, hipStream_t stream, std::string& err);
+  int (*traj)(const DevCfg& c, const DevState& s, const float* params, float* dpos, float* dvel, hipStream_t stream,
+              std::string& err);
+  int (*traj_env)(const DevCfg& c, const DevState& s, const float* params, float* env_tab, float* dpos, float* dvel,
+                  int32_t* plan_len, float* info_pos, float* info_vel, hipStream_t stream, std::string& err);
+};
+}  // namespace fgx
+const fgx::NlOps* fgx_nl_ops_1();
+const fgx::NlOps* fgx_nl_ops_3();
+const fgx::NlOps* fgx_nl_ops_4();
+const fgx::NlOps* fgx_nl_ops_6();
+const fgx::NlOps* fgx_nl_ops_7();
+const fgx::NlOps* fgx_nl_ops_8();
+
+namespace fgx {
 
 // Episode kernels: k_episode (fgx_kernels.h, one env per lane, every case), k_episode_jl (fgx_jl.h,
 // one lane per env x joint), k_episode_jp (fgx_jp.h, one wave per joint) and k_episode_ws
@@ -142,14 +167,17 @@ static int launch_ws(const DevCfg& c, const DevState& s, const float* params, co
   return 0;
 }
 
-template <int ENV, int MP, int CTRL, int NL, int NB>
+// LOG_ONLY (n_links outside {2, 5}, fgx_ep_nl.h): only the logging k_episode is instantiated; it
+// serves every info level (no per-step array given: nothing is staged or stored) and the validity
+// checks, so each further link count costs one kernel per (env, MP, controller), not a family.
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG_ONLY = false>
 static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* params, const float* dpos,
                              const float* dvel, const Outputs& o, hipStream_t stream, std::string& err) {
   const int threads = 256;
   const int blocks = (int)((c.N + threads - 1) / threads);
   const size_t lds = (MP == MP_GIVEN) ? 0 : (size_t)c.rows * c.stride * sizeof(float);
   // the logging instantiation also runs the trajectory-validity checks (c.valid_flags)
-  const bool log = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided ||
+  const bool log = LOG_ONLY || o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided ||
                    o.end_effector || o.reward_dist || c.valid_flags != 0;
   if constexpr (MP != MP_GIVEN && NB != 0) {
     if (c.stride != Traj<MP, 1, NB>::KS) {
@@ -157,13 +185,13 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
       return -1;
     }
   }
-  if constexpr (ENV == ENV_SIMPLE && MP != MP_GIVEN && CTRL == CTRL_PD) {
+  if constexpr (!LOG_ONLY && ENV == ENV_SIMPLE && MP != MP_GIVEN && CTRL == CTRL_PD) {
     const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);
   }
-  if constexpr (ENV == ENV_HOLE && NL == 5) {
+  if constexpr (!LOG_ONLY && ENV == ENV_HOLE && NL == 5) {
     if (classic_choice(c, log) == EK_PAIR) {
       const int pblocks = (int)((2 * c.N + threads - 1) / threads);
       hipLaunchKernelGGL((k_episode_pair<ENV, MP, CTRL, NL, NB>), dim3(pblocks), dim3(threads), lds, stream, c, s,
@@ -173,7 +201,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
       return 0;
     }
   }
-  if constexpr (ENV == ENV_SIMPLE && NL == 5) {
+  if constexpr (!LOG_ONLY && ENV == ENV_SIMPLE && NL == 5) {
     if (classic_choice(c, log) == EK_CLASSIC_W2 &&
         (MP == MP_GIVEN || CTRL != CTRL_PD || episode_kernel_choice(c, MP, log, s.plan_len != nullptr) == EK_CLASSIC_W2)) {
       hipLaunchKernelGGL((k_episode_w2<ENV, MP, CTRL, NL, NB, false>), dim3(blocks), dim3(threads), lds, stream, c,
@@ -206,7 +234,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
       }
     }
   }
-  else
+  else if constexpr (!LOG_ONLY)
     hipLaunchKernelGGL((k_episode<ENV, MP, CTRL, NL, NB, false>), dim3(blocks), dim3(threads), lds, stream, c, s,
                        params, dpos, dvel, o);
   const hipError_t e = hipGetLastError();
@@ -214,37 +242,46 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
   return 0;
 }
 
-template <int ENV, int MP, int CTRL, int NB>
+// NLV > 0: that link count only (the per-link-count units of fgx_ep_nl.h, logging kernel only);
+// NLV = 0: the registered 2 and 5
+template <int ENV, int MP, int CTRL, int NB, int NLV = 0>
 static int launch_episode_ctrl(const DevCfg& c, const DevState& s, const float* params, const float* dpos,
                                const float* dvel, const Outputs& o, hipStream_t stream, std::string& err) {
-  if (c.nl == 2) return launch_episode_nl<ENV, MP, CTRL, 2, NB>(c, s, params, dpos, dvel, o, stream, err);
-  if (c.nl == 5) return launch_episode_nl<ENV, MP, CTRL, 5, NB>(c, s, params, dpos, dvel, o, stream, err);
-  err = "n_links not instantiated (supported: 2, 5)";
+  if constexpr (NLV > 0) {
+    if (c.nl == NLV) return launch_episode_nl<ENV, MP, CTRL, NLV, NB, true>(c, s, params, dpos, dvel, o, stream, err);
+  } else {
+    if (c.nl == 2) return launch_episode_nl<ENV, MP, CTRL, 2, NB>(c, s, params, dpos, dvel, o, stream, err);
+    if (c.nl == 5) return launch_episode_nl<ENV, MP, CTRL, 5, NB>(c, s, params, dpos, dvel, o, stream, err);
+  }
+  err = "n_links not instantiated in this unit";
   return -4;
 }
 
-template <int ENV, int MP, int NB>
+template <int ENV, int MP, int NB, int NLV = 0>
 static int launch_episode_mp(const DevCfg& c, const DevState& s, const float* params, const float* dpos,
                              const float* dvel, const Outputs& o, hipStream_t stream, std::string& err) {
   switch (c.ctrl) {
-    case CTRL_PD: return launch_episode_ctrl<ENV, MP, CTRL_PD, NB>(c, s, params, dpos, dvel, o, stream, err);
-    case CTRL_VEL: return launch_episode_ctrl<ENV, MP, CTRL_VEL, NB>(c, s, params, dpos, dvel, o, stream, err);
-    case CTRL_POS: return launch_episode_ctrl<ENV, MP, CTRL_POS, NB>(c, s, params, dpos, dvel, o, stream, err);
+    case CTRL_PD: return launch_episode_ctrl<ENV, MP, CTRL_PD, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
+    case CTRL_VEL: return launch_episode_ctrl<ENV, MP, CTRL_VEL, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
+    case CTRL_POS: return launch_episode_ctrl<ENV, MP, CTRL_POS, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
   }
   err = "bad ctrl_kind";
   return -1;
 }
 
-// NB = 5: every MP kind and the caller-given trajectory; NB = 0: the MP kinds with c.nb != 5
-template <int ENV, int NB>
+// NB = 5: every MP kind and the caller-given trajectory; NB = 0: the MP kinds with c.nb != 5 (and,
+// in the per-link-count units NLV > 0, every basis count and the caller-given trajectory)
+template <int ENV, int NB, int NLV = 0>
 static int launch_episode_env(const DevCfg& c, const DevState& s, int mp, const float* params, const float* dpos,
                               const float* dvel, const Outputs& o, hipStream_t stream, std::string& err) {
   switch (mp) {
-    case MP_PROMP: return launch_episode_mp<ENV, MP_PROMP, NB>(c, s, params, dpos, dvel, o, stream, err);
-    case MP_DMP: return launch_episode_mp<ENV, MP_DMP, NB>(c, s, params, dpos, dvel, o, stream, err);
-    case MP_PRODMP: return launch_episode_mp<ENV, MP_PRODMP, NB>(c, s, params, dpos, dvel, o, stream, err);
+    case MP_PROMP: return launch_episode_mp<ENV, MP_PROMP, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
+    case MP_DMP: return launch_episode_mp<ENV, MP_DMP, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
+    case MP_PRODMP: return launch_episode_mp<ENV, MP_PRODMP, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
     case MP_GIVEN:
-      if (NB == 5) return launch_episode_mp<ENV, MP_GIVEN, 5>(c, s, params, dpos, dvel, o, stream, err);
+      // (if constexpr: the NB = 0 units of 2 / 5 links do not compile a second caller-given family)
+      if constexpr (NB == 5 || NLV > 0)
+        return launch_episode_mp<ENV, MP_GIVEN, NB, NLV>(c, s, params, dpos, dvel, o, stream, err);
       break;
   }
   err = "bad mp kind";

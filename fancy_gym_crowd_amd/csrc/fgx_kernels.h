@@ -454,17 +454,10 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
       v.qd[d] = fadd(v.qd[d], inc);
       v.q[d] = fadd(v.q[d], c.dt * v.qd[d]);
     }
+    // np.sum(np.square(action)) (simple_reacher.py:60-62): f32 for a float32 action array
     double ctrl;
-    if (F32) {
-      float s32 = a32[0] * a32[0];
-#pragma unroll
-      for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
-      ctrl = (double)s32;
-    } else {
-      ctrl = a[0] * a[0];
-#pragma unroll
-      for (int d = 1; d < NL; ++d) ctrl = fadd(ctrl, a[d] * a[d]);
-    }
+    if (F32) ctrl = (double)np_sum<NL, float>([&](int d) { return a32[d] * a32[d]; }, [](float x, float y) { return x + y; });
+    else ctrl = np_sum<NL, double>([&](int d) { return a[d] * a[d]; }, [](double x, double y) { return fadd(x, y); });
     // MAYFK = false: the caller guarantees st < 199 (fast blocks), no FK code in the loop body
     if (MAYFK && (st >= 199 || fk_always)) v.fk();
     if (MAYFK && st >= 199) r.rdist = -norm2(v.jx[NL] - v.gx, v.jy[NL] - v.gy);
@@ -473,20 +466,23 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
   } else {   // direct velocity control: HoleReacher, ViaPointReacher
     double acc_cost = 0.0;
     if (ENV == ENV_HOLE) {   // ViaPointReacher's reward uses the action, not _acc
+      // np.sum(self._acc ** 2) (hr_simple_reward.py:48 and the other reward functions)
       if (F32 && (v.flags & 1u)) {   // qd already holds a float32 array: f32 arithmetic
-        float s32 = 0.0f;
+        float sq[NL];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
           const float ac = div_rcp(a32[d] - (float)v.qd[d], c.dt32, c.rcp_dt32);
-          s32 = (d == 0) ? ac * ac : s32 + ac * ac;
+          sq[d] = ac * ac;
         }
-        acc_cost = (double)s32;
+        acc_cost = (double)np_sum<NL, float>([&](int d) { return sq[d]; }, [](float x, float y) { return x + y; });
       } else {
+        double sq[NL];
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
           const double ac = div_rcp64(a[d] - v.qd[d], c.dt, c.rcp_dt);
-          acc_cost = (d == 0) ? ac * ac : acc_cost + ac * ac;
+          sq[d] = ac * ac;
         }
+        acc_cost = np_sum<NL, double>([&](int d) { return sq[d]; }, [](double x, double y) { return x + y; });
       }
     }
 #pragma unroll
@@ -499,17 +495,9 @@ __device__ __forceinline__ StepOut substep(const DevCfg& c, Env<NL>& v, const do
     if constexpr (PAIR) v.fk_pair(pp);
     else v.fk();
     // sum(action**2) == sum(qd**2) after the step (f32 for a float32 action array)
-    double act_sq;
-    if (F32) {
-      float s32 = a32[0] * a32[0];
-#pragma unroll
-      for (int d = 1; d < NL; ++d) s32 = s32 + a32[d] * a32[d];
-      act_sq = (double)s32;
-    } else {
-      act_sq = a[0] * a[0];
-#pragma unroll
-      for (int d = 1; d < NL; ++d) act_sq = act_sq + a[d] * a[d];
-    }
+    const double act_sq =
+        F32 ? (double)np_sum<NL, float>([&](int d) { return a32[d] * a32[d]; }, [](float x, float y) { return x + y; })
+            : np_sum<NL, double>([&](int d) { return a[d] * a[d]; }, [](double x, double y) { return x + y; });
     if (ENV == ENV_VIA) {   // viapoint_reacher.py:79-111
       r.coll = c.allow_self ? false : self_c();
       // 5e-8 * np.sum(action**2): a float32 sum stays float32 (NEP 50)

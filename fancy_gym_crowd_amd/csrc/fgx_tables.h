@@ -1,9 +1,13 @@
-// fgx_tables.h — basis-table kernels (included by fgx_api.hip only).
-//   k_tables_rbf     ProMP / DMP rows: normalized-RBF basis on the phase of t_i = i*dt
-//   k_tables_prodmp  ProDMP precompute: cumulative-trapezoid integrals + homogeneous solutions
-// All values are computed in f64 and rounded once to f32 (oracle/mp.py:build_tables).
+// fgx_tables.h — basis-table device functions (the kernels that run them once per handle are in
+// fgx_tables_k.h; k_traj_env builds per-env rows with the same functions, fgx_learned.h):
+//   rbf_row          ProMP / DMP rows: normalized-RBF basis on the phase of t_i = i*dt
+//   prodmp_*         ProDMP precompute: cumulative-trapezoid integrals + homogeneous solutions
+// All values are computed in f64 and rounded once to f32 (oracle/mp.py:build_tables); every exp is
+// fgx_exp (fgx_exp.h), which oracle/mp.py:exp64 restates operation for operation, so the tables
+// equal the oracle's bit for bit.
 #pragma once
 #include "fgx_device.h"
+#include "fgx_exp.h"
 
 namespace fgx {
 
@@ -12,7 +16,7 @@ __device__ inline double phase64(const DevCfg& c, double t, double tau, double d
   double lin = (t - delay) / tau;
   lin = lin > 0.0 ? lin : 0.0;   // np.maximum(x, 0.0)
   if (c.phase == 0) return lin < 1.0 ? lin : 1.0;
-  return exp((-alpha_x) * lin);
+  return fgx_exp((-alpha_x) * lin);
 }
 
 // normalized RBF at phase x, f64, all n = nb + zs + zg columns (oracle/mp.py:rbf64); centres at the
@@ -23,13 +27,13 @@ __device__ inline void rbf64(const DevCfg& c, double alpha_x, double bw, double 
   double cen[kMaxBasis + 4], e[kMaxBasis + 4];
   for (int j = 0; j < n; ++j) {
     const double u = (n > 1) ? (double)(j - c.nbo) / (double)(n - 2 * c.nbo - 1) : 0.0;
-    cen[j] = (c.phase == 0) ? u : exp((-alpha_x) * u);
+    cen[j] = (c.phase == 0) ? u : fgx_exp((-alpha_x) * u);
   }
   for (int j = 0; j < n; ++j) {
     double d = (n > 1) ? ((j < n - 1) ? cen[j + 1] - cen[j] : cen[n - 1] - cen[n - 2]) : 1.0;
     const double h = bw / (d * d);
     const double dd = x - cen[j];
-    e[j] = exp((-h) * (dd * dd) / 2);
+    e[j] = fgx_exp((-h) * (dd * dd) / 2);
   }
   double s;
   if (n < 8) {
@@ -69,21 +73,14 @@ __device__ inline void rbf_row(const DevCfg& c, int i, double tau, double delay,
   }
 }
 
-// ProMP / DMP tables: one thread per row.
-__global__ void k_tables_rbf(DevCfg c, double tau, double delay, double alpha_x, double bw, float* tab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.rows) return;
-  rbf_row(c, i, tau, delay, alpha_x, bw, tab + (size_t)i * c.stride);
-}
-
 // ProDMP fine-grid pieces at s = i*h (oracle/mp.py:prodmp_fine64): the variation-of-parameters
 // integrands k1*phi, k2*phi and the homogeneous solutions.
 __device__ inline void prodmp_integrands(const DevCfg& c, double s, double alpha_x, double bw, double* d1,
                                          double* d2) {
-  const double x = exp((-alpha_x) * s);
+  const double x = fgx_exp((-alpha_x) * s);
   double phi[kMaxBasis + 4];
   rbf64(c, alpha_x, bw, x, phi);
-  const double e = exp(c.alpha * s / 2);
+  const double e = fgx_exp(c.alpha * s / 2);
   const double k1 = s * e * x, k2 = e * x;
   for (int j = 0; j < c.nb; ++j) {
     d1[j] = k1 * phi[c.zs + j];
@@ -95,8 +92,8 @@ __device__ inline void prodmp_integrands(const DevCfg& c, double s, double alpha
 __device__ inline void prodmp_row(const DevCfg& c, double s, const double* p1, const double* p2, float* row) {
   const int nb = c.nb;
   const double a = c.alpha;
-  const double e = exp(a * s / 2);
-  const double y1 = exp((-a) * s / 2);
+  const double e = fgx_exp(a * s / 2);
+  const double y1 = fgx_exp((-a) * s / 2);
   const double y2 = s * y1;
   const double dy1 = -a / 2 * y1;
   const double dy2 = -a / 2 * y2 + y1;
@@ -114,84 +111,52 @@ __device__ inline void prodmp_row(const DevCfg& c, double s, const double* p1, c
   row[2 * nb + 5] = (float)dy2;
 }
 
-// ProDMP with a delay: the basis is looked up on the left-bounded linear phase, fine-grid index
-// j(i) = rint(max((t_i - delay) / tau, 0) / (dt / tau)) for t_i = i dt (oracle/mp.py:
-// prodmp_delay_index): rows before the delay all equal the s = 0 row, so the plan holds its
-// initial position and velocity there (test_black_box.py:267-307).  j(i) <= i, non-decreasing.
-__device__ inline int prodmp_delay_index(const DevCfg& c, int i, double tau, double delay) {
-  double u = ((double)i * c.dt - delay) / tau;
+// ProDMP with a delay or a basis dt of its own (basis_generator_kwargs dt,
+// basis_generator_factory.py:8-23): the basis is looked up on the left-bounded linear phase, fine-grid
+// index j(i) = rint(max((t_i - delay) / tau, 0) / (bdt / tau)) for t_i = i dt (oracle/mp.py:
+// prodmp_delay_index): rows before the delay all equal the s = 0 row, so the plan holds its initial
+// position and velocity there (test_black_box.py:267-307).  j(i) is non-decreasing in i; without a
+// delay and with bdt = dt it is i (prodmp_identity: no lookup).  jmax clamps a non-finite value.
+__host__ __device__ inline bool prodmp_identity(double delay, double dt, double bdt) { return delay == 0.0 && bdt == dt; }
+__host__ __device__ inline int prodmp_delay_index(double dt, double bdt, int i, double tau, double delay, int jmax) {
+  double u = ((double)i * dt - delay) / tau;
   u = u > 0.0 ? u : 0.0;                       // (NaN -> 0)
-  // j <= i holds for every delay >= 0 (fgx_create refuses a negative or non-finite static delay,
-  // learned delays are clipped to delay_bound, lo >= 0); the clamp keeps any other value inside
-  // the rows already computed
-  const double j = rint(u / (c.dt / tau));
-  return j < (double)i ? (int)j : i;
+  const double j = __builtin_rint(u / (bdt / tau));
+  return j < (double)jmax ? (j > 0.0 ? (int)j : 0) : jmax;
+}
+// fine-grid rows the shared table needs: j(rows - 1) + 1 (host: scratch size; device: the grid)
+__host__ __device__ inline int prodmp_fine_rows(double dt, double bdt, int rows, double tau, double delay) {
+  if (prodmp_identity(delay, dt, bdt)) return rows;
+  return prodmp_delay_index(dt, bdt, rows - 1, tau, delay, 1 << 24) + 1;
 }
 
-// One env's ProDMP rows 0..R-1 for its own tau, sequentially in one thread (the cumulative
-// trapezoid in the same order as k_tables_prodmp / the oracle), then the delay remap in place
-// (descending i: row j(i) <= i is still the fine-grid row when row i is written).
+// One env's ProDMP rows 0..R-1 for its own tau, sequentially in one thread: the cumulative
+// trapezoid walks the fine grid in the same order as k_tables_prodmp / the oracle, and row i is
+// emitted when the walk reaches fine-grid row j(i) (non-decreasing in i).  jmax: the walk's bound.
 __device__ inline void prodmp_rows_seq(const DevCfg& c, double tau, double delay, double alpha_x, double bw, int R,
                                        float* tab) {
   const int nb = c.nb;
-  const double h = c.dt / tau;
+  const double h = c.bdt / tau;
+  const bool ident = prodmp_identity(delay, c.dt, c.bdt);
+  const int jmax = ident ? R - 1 : prodmp_delay_index(c.dt, c.bdt, R - 1, tau, delay, 1 << 20);
   double p1[kMaxBasis], p2[kMaxBasis], prev1[kMaxBasis], prev2[kMaxBasis], cur1[kMaxBasis], cur2[kMaxBasis];
   prodmp_integrands(c, 0.0, alpha_x, bw, prev1, prev2);
   for (int j = 0; j < nb; ++j) { p1[j] = 0.0; p2[j] = 0.0; }
-  prodmp_row(c, 0.0, p1, p2, tab);
-  for (int i = 1; i < R; ++i) {
-    const double s = (double)i * h;
-    prodmp_integrands(c, s, alpha_x, bw, cur1, cur2);
-    for (int j = 0; j < nb; ++j) {
-      p1[j] = p1[j] + h * (prev1[j] + cur1[j]) / 2;
-      p2[j] = p2[j] + h * (prev2[j] + cur2[j]) / 2;
-      prev1[j] = cur1[j];
-      prev2[j] = cur2[j];
+  int f = 0;   // fine-grid row of p1 / p2
+  for (int i = 0; i < R; ++i) {
+    const int ji = ident ? i : prodmp_delay_index(c.dt, c.bdt, i, tau, delay, jmax);
+    for (; f < ji; ++f) {
+      const double s = (double)(f + 1) * h;
+      prodmp_integrands(c, s, alpha_x, bw, cur1, cur2);
+      for (int j = 0; j < nb; ++j) {
+        p1[j] = p1[j] + h * (prev1[j] + cur1[j]) / 2;
+        p2[j] = p2[j] + h * (prev2[j] + cur2[j]) / 2;
+        prev1[j] = cur1[j];
+        prev2[j] = cur2[j];
+      }
     }
-    prodmp_row(c, s, p1, p2, tab + (size_t)i * c.stride);
+    prodmp_row(c, (double)f * h, p1, p2, tab + (size_t)i * c.stride);
   }
-  if (delay != 0.0)
-    for (int i = R - 1; i > 0; --i) {
-      const int j = prodmp_delay_index(c, i, tau, delay);
-      if (j != i)
-        for (int k = 0; k < c.stride; ++k) tab[(size_t)i * c.stride + k] = tab[(size_t)j * c.stride + k];
-    }
-}
-
-// ProDMP precompute (oracle/mp.py:prodmp_fine64).  Single block; scratch: [rows][2*nb] f64.
-__global__ void k_tables_prodmp(DevCfg c, double tau, double delay, double alpha_x, double bw, double* dp,
-                                float* tab) {
-  const int nb = c.nb, R = c.rows, W = 2 * nb;
-  const double h = c.dt / tau;
-  for (int i = threadIdx.x; i < R; i += blockDim.x)
-    prodmp_integrands(c, (double)i * h, alpha_x, bw, dp + (size_t)i * W, dp + (size_t)i * W + nb);
-  __syncthreads();
-  // cumulative trapezoid, one thread per column, sequential (same order as the oracle)
-  if ((int)threadIdx.x < W) {
-    const int j = threadIdx.x;
-    double p = 0.0, prev = dp[j];
-    dp[j] = 0.0;
-    for (int i = 1; i < R; ++i) {
-      const double cur = dp[(size_t)i * W + j];
-      p = p + h * (prev + cur) / 2;
-      dp[(size_t)i * W + j] = p;
-      prev = cur;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {   // row i = fine-grid row j(i) (delay)
-    const int j = delay != 0.0 ? prodmp_delay_index(c, i, tau, delay) : i;
-    prodmp_row(c, (double)j * h, dp + (size_t)j * W, dp + (size_t)j * W + nb, tab + (size_t)i * c.stride);
-  }
-}
-
-// column-major copy of the shared table (DevState::tables_t)
-__global__ void k_tables_transpose(int rows, int stride, int nb, const float* tab, float* tt) {
-  const int RT = tables_t_rows(rows);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= stride * RT) return;
-  const int col = i / RT, r = i - col * RT - tables_t_pad(col, nb);
-  tt[i] = (r >= 0 && r < rows) ? tab[(size_t)r * stride + col] : 0.0f;
 }
 
 }  // namespace fgx

@@ -385,6 +385,13 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     c = _lib.FgxConfig()
     c.abi_version = _lib.FGX_ABI_VERSION
     n = int(kw['n_links'])
+    if not 1 <= n <= 8:   # the engine's register-resident joint arrays (include/fgx.h n_links 1..8)
+        raise ValueError(f"n_links must be in 1..8, got {n}")
+    if spec.kind == 'hole' and n == 1 and not kw.get('allow_wall_collision', False):
+        # the reference's wall check indexes np.squeeze(line_points) as [link, point, xy]; one link
+        # squeezes to [point, xy] and its first step raises (hole_reacher.py:126-148)
+        raise IndexError("too many indices for array: HoleReacher with n_links=1 cannot run its wall check "
+                         "(hole_reacher.py:143); pass allow_wall_collision=True")
     c.n_links = n
     c.env_kind = {'simple': _lib.ENV_SIMPLE, 'hole': _lib.ENV_HOLE, 'via': _lib.ENV_VIA}[spec.kind]
     # constructor defaults: SimpleReacherEnv random_start=True; HoleReacherEnv / ViaPointReacherEnv False
@@ -517,9 +524,14 @@ def resolve(env_id, mp_config_override=None, **env_kwargs):
     if tg_type == 'prodmp':
         c.alpha = float(bs.get('alpha', D['prodmp_alpha']))
         c.pc_length = float(bs.get('pre_compute_length_factor', D['pre_compute_length_factor']))
-        if float(bs.get('dt', c.dt)) != c.dt:
-            raise NotImplementedError("ProDMP basis dt different from the env dt")
+        # the ProDMP basis generator's own dt (its precompute grid, basis_generator_factory.py:8-23);
+        # rows are looked up at the rounded grid index of each env step (fgx_tables.h)
+        c.basis_dt = float(bs.get('dt', c.dt))
+        if not (c.basis_dt > 0.0):
+            raise ValueError("basis generator dt must be positive")
     else:
+        if 'dt' in bs:   # NormalizedRBF / ZeroPadding generators take no dt (mp_pytorch constructors)
+            raise TypeError(f"{bs_type} basis generator got an unexpected keyword argument 'dt'")
         c.alpha = float(tg.get('alpha', D['dmp_alpha']))
         c.pc_length = D['pre_compute_length_factor']
     # PDController(p_gains, d_gains) (pd_controller.py:16-29): scalars or one gain per joint

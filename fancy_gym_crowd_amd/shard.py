@@ -57,3 +57,12 @@ def gather_ints(values, device, group=None):
     parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
     dist.all_gather(parts, t, group=group)
     return [[int(x) for x in p.tolist()] for p in parts]
+
+
+def gather_floats(values, device, group=None):
+    """all_gather a short list of floats from every rank -> [world][len(values)] (rank order)."""
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [[float(x) for x in p.tolist()] for p in parts]

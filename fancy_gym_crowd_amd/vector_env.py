@@ -344,20 +344,25 @@ class BlackBoxVectorEnv:
 
     # ------------------------------------------------------------------ fast path (bench)
     def step_into(self, actions, obs, ret, te, tr, tl, fobs=None, inner_steps=None):
-        """Allocation-free BB step into preallocated buffers (no argument checks; for benchmarks).
-        inner_steps: optional zero-initialised int64 [_lib.INNER_STEPS_LEN] device partial counters
-        (new_inner_steps() allocates them): their sum += the sum of trajectory lengths."""
+        """Allocation-free BB step into preallocated buffers (no shape checks of the env buffers; for
+        benchmarks).  inner_steps: optional zero-initialised int64 [_lib.INNER_STEPS_LEN] device
+        partial counters (new_inner_steps() allocates them): their sum += the sum of trajectory
+        lengths.  A failed launch raises (fgx_step's return code is checked)."""
         _order_check(self)
         info = None
         if inner_steps is not None:
+            # the kernels add to line (wave % 128) * 16 of the array: a shorter one would be written past
+            if inner_steps.dtype != torch.int64 or inner_steps.numel() < _lib.INNER_STEPS_LEN:
+                raise ValueError(f"inner_steps must be int64 with >= {_lib.INNER_STEPS_LEN} entries (new_inner_steps())")
             info = _lib.FgxInfo()
             info.inner_steps = inner_steps.data_ptr()
             info = ctypes.byref(info)
-        self._eng.lib.fgx_step(self._eng.h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
-                               ctypes.c_void_p(ret.data_ptr()), ctypes.c_void_p(te.data_ptr()),
-                               ctypes.c_void_p(tr.data_ptr()), ctypes.c_void_p(tl.data_ptr()),
-                               ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, info,
-                               int(self.autoreset), self._eng.stream())
+        _lib.check(self._eng.lib.fgx_step(self._eng.h, ctypes.c_void_p(actions.data_ptr()),
+                                          ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(ret.data_ptr()),
+                                          ctypes.c_void_p(te.data_ptr()), ctypes.c_void_p(tr.data_ptr()),
+                                          ctypes.c_void_p(tl.data_ptr()),
+                                          ctypes.c_void_p(fobs.data_ptr()) if fobs is not None else None, info,
+                                          int(self.autoreset), self._eng.stream()))
 
     def new_inner_steps(self):
         """Zeroed device partial counters for step_into(inner_steps=...); total = .sum()."""

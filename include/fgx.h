@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define FGX_ABI_VERSION 7
+#define FGX_ABI_VERSION 8
 
 /* error codes */
 #define FGX_OK 0
@@ -107,7 +107,8 @@ extern "C" {
 typedef struct fgx_config {
   int32_t abi_version;          /* = FGX_ABI_VERSION                                        */
   int32_t env_kind;             /* FGX_ENV_*                                                */
-  int32_t n_links;              /* 1..8                                                     */
+  int32_t n_links;              /* 1..8 (2 and 5, the registered reachers, have specialised 
+                                   kernels; 1, 3, 4, 6, 7, 8 run the logging k_episode)       */
   int32_t random_start;         /* base_reacher.py:81-86                                    */
   int32_t allow_self_collision; /* HoleReacher only                                         */
   int32_t allow_wall_collision; /* HoleReacher only                                         */
@@ -166,6 +167,10 @@ typedef struct fgx_config {
   double invalid_reward;
   double valid_tau_lo, valid_tau_hi, valid_delay_lo, valid_delay_hi;
   double valid_pos_lo[8], valid_pos_hi[8];
+  /* ---- ABI 8 */
+  double basis_dt;              /* ProDMP basis generator dt (basis_generator_kwargs 'dt',
+                                   basis_generator_factory.py:8-23): step of the precompute grid
+                                   s_j = j * basis_dt / tau; 0 = the env dt                    */
 } fgx_config;
 
 typedef struct fgx_dims {

@@ -17,15 +17,18 @@ DT32 = f32(0.01)
 
 
 def _seqsum(sq, as32):
-    """np.sum over the last axis of a [N, n<8] array: left-to-right (f32 when as32)."""
-    if as32:
-        c = sq[:, 0].astype(f32)
-        for j in range(1, sq.shape[1]):
-            c = (c + sq[:, j]).astype(f32)
-        return c
-    c = sq[:, 0] + 0.0
-    for j in range(1, sq.shape[1]):
-        c = c + sq[:, j]
+    """np.sum over the last axis of a [N, n <= 8] array in numpy's pairwise_sum order (umath
+    loops_utils.h): left to right for n < 8, at n = 8 the eight accumulators combined as
+    ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) (f32 when as32)."""
+    n = sq.shape[1]
+    dt = f32 if as32 else np.float64
+    if n == 8:
+        r = [sq[:, j].astype(dt) for j in range(8)]
+        return (((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))).astype(dt)
+    assert n < 8
+    c = sq[:, 0].astype(f32) if as32 else sq[:, 0] + 0.0
+    for j in range(1, n):
+        c = (c + sq[:, j]).astype(dt)
     return c
 
 
@@ -171,16 +174,9 @@ class BatchedReacher:
         steps = self.steps
         if self.kind == "simple":
             if a_is_f32:
-                sq = (a.astype(f32) ** 2)
-                ctrl = sq[:, 0].astype(f32)
-                for j in range(1, n):
-                    ctrl = (ctrl + sq[:, j]).astype(f32)
-                ctrl = ctrl.astype(np.float64)
+                ctrl = _seqsum(a.astype(f32) ** 2, True).astype(np.float64)
             else:
-                sq = a ** 2
-                ctrl = sq[:, 0] + 0.0
-                for j in range(1, n):
-                    ctrl = ctrl + sq[:, j]
+                ctrl = _seqsum(a ** 2, False)
             dist = np.zeros(N)
             need = act & (steps >= 199)
             if np.any(need):

@@ -21,7 +21,8 @@ basis       normalized RBF, centres = unbounded phase of linspace(delay - o d, d
             zero padding builds n_b + z_s + z_g RBFs and keeps columns z_s..z_s+n_b-1
             [factory/basis_generator_factory.py:10-17]
 tables      every table value is computed in f64 and rounded once to f32 (mp_pytorch computes
-            in torch f32 on the CPU; f64-then-round is the deliberate, documented choice)
+            in torch f32 on the CPU; f64-then-round is the deliberate, documented choice), with
+            exp64 (= csrc/fgx_exp.h) as the exp, so the device tables equal these bit for bit
 ProMP       pos_k[d] = fma-chain_j(Phi[i][j], w[d][j]) with Phi = f32(weights_scale*phi);
             vel_k = f32(f32(pos_{k+1}-pos_k) / dt32_i), dt32_i = f32(f32(t_{i+1}) - f32(t_i)),
             vel_{T-1} = vel_{T-2}.  params = w, dof-major (w[d][j] = params[d*n_b + j]).
@@ -31,8 +32,8 @@ DMP         tau^2 y'' = alpha(beta(g-y) - tau y') + f, beta = alpha/4, f = x*phi
             y_0 = f32(q0), z_0 = f32(f32(qd0)*tau).  params = [w (dof-major), g (dof)].
 ProDMP      q(s) = c1 y1(s) + c2 y2(s) + Phi_p(s).[w; g], y1 = exp(-alpha s/2), y2 = s y1,
             Phi_p/Phi_v from the cumulative-trapezoid variation-of-parameters integrals on the
-            grid s_j = j*dt/tau up to s = 6 (pre_compute_length_factor), looked up at the
-            rounded grid index; (c1, c2) solved from q(s0) = q0, q'(s0) = tau*qd0 (2x2
+            grid s_j = j*bdt/tau up to s = 6 (pre_compute_length_factor; bdt = the basis
+            generator's dt, default the env dt), looked up at the rounded grid index; (c1, c2) solved from q(s0) = q0, q'(s0) = tau*qd0 (2x2
             Wronskian).  params = per-dof blocks [w_d (n_b), g_d] (num_basis_g = n_b + 1).
 """
 from dataclasses import dataclass, field, replace
@@ -65,6 +66,11 @@ class MPSpec:
     duration: float = 2.0
     extra: dict = field(default_factory=dict)
     T_override: int = 0            # learn_sub_trajectories: T = round(tau / dt) per env
+    basis_dt: float = 0.0          # ProDMP basis generator dt (its precompute grid); 0 = the env dt
+
+    @property
+    def bdt(self):
+        return self.basis_dt or self.dt
 
     @property
     def T(self):
@@ -77,12 +83,46 @@ class MPSpec:
         return self.dof * (self.n_basis + 1)
 
 
+# ----------------------------------------------------------------------------- exp of the tables
+_L2E = 1.4426950408889634
+_LN2_HI = 6.93147180369123816490e-01
+_LN2_LO = 1.90821492927058770002e-10
+_EXP_C = [1.6059043836821613e-10, 2.08767569878681e-09, 2.505210838544172e-08, 2.755731922398589e-07,
+          2.7557319223985893e-06, 2.48015873015873e-05, 0.0001984126984126984, 0.001388888888888889,
+          0.008333333333333333, 0.041666666666666664, 0.16666666666666666, 0.5]
+
+
+def exp64(x):
+    """The tables' exp (csrc/fgx_exp.h:fgx_exp), operation for operation: Cody-Waite reduction with
+    fdlibm's two-part ln 2, degree-13 Taylor polynomial in Horner form with separate IEEE mul / add
+    (numpy ufuncs never fuse), exact scaling by 2^k (subnormal results: exact ldexp, then one
+    multiplication by 2^-600).  Deterministic on both sides, so device tables == oracle tables bit
+    for bit; a few f64 ulp from the true exp (the tables then round to f32).  mp_pytorch itself
+    evaluates torch f32 exp: parity to it stays unpinned either way."""
+    x = np.asarray(x, np.float64)
+    with np.errstate(over="ignore", invalid="ignore"):
+        xs = np.where(np.isfinite(x), np.clip(x, -746.0, 709.8), 0.0)
+        k = np.rint(xs * _L2E)
+        r = (xs - k * _LN2_HI) - k * _LN2_LO
+        p = np.full_like(r, _EXP_C[0])
+        for c in _EXP_C[1:]:
+            p = p * r + c
+        p = p * r + 1.0
+        p = p * r + 1.0
+        ki = k.astype(np.int32)
+        small = ki < -1000
+        y = np.where(small, np.ldexp(p, np.where(small, ki + 600, 0)) * 2.0 ** -600, np.ldexp(p, np.where(small, 0, ki)))
+    y = np.where(x > 709.8, np.inf, y)
+    y = np.where(x < -746.0, 0.0, y)
+    return np.where(np.isnan(x), x, y)
+
+
 # ----------------------------------------------------------------------------- phase / basis
 def phase64(spec, t):
     lin = np.maximum((np.asarray(t, np.float64) - spec.delay) / spec.tau, 0.0)
     if spec.phase == "linear":
         return np.minimum(lin, 1.0)
-    return np.exp(-spec.alpha_phase * lin)
+    return exp64(-spec.alpha_phase * lin)
 
 
 def centers64(spec):
@@ -90,7 +130,7 @@ def centers64(spec):
     o = spec.basis_outside                # centres at the unbounded phase of
     # linspace(delay - o d, delay + tau + o d, n), d = tau / (n - 2o - 1): u_j = (j - o) / (n - 2o - 1)
     u = (np.arange(n, dtype=np.float64) - o) / (n - 2 * o - 1) if n > 1 else np.zeros(1)
-    c = u if spec.phase == "linear" else np.exp(-spec.alpha_phase * u)
+    c = u if spec.phase == "linear" else exp64(-spec.alpha_phase * u)
     if n > 1:
         d = np.empty(n)
         d[:-1] = c[1:] - c[:-1]
@@ -116,22 +156,23 @@ def rbf64(spec, x):
     """Normalized RBF values in f64, zero-padding columns removed: [..., n_basis]."""
     c, h = centers64(spec)
     d = np.asarray(x, np.float64)[..., None] - c
-    e = np.exp((-h) * (d * d) / 2)
+    e = exp64((-h) * (d * d) / 2)
     phi = e / _seqsum_last(e)[..., None]
     return phi[..., spec.zero_start:spec.zero_start + spec.n_basis]
 
 
 # ----------------------------------------------------------------------------- tables
 def prodmp_fine64(spec, n_rows):
-    """ProDMP precompute on the fine grid s_j = j*dt/tau (f64), rows 0..n_rows-1."""
-    h = spec.dt / spec.tau
+    """ProDMP precompute on the fine grid s_j = j*bdt/tau (f64), rows 0..n_rows-1 (bdt: the basis
+    generator's dt, basis_generator_factory.py:8-23 passes it through; default the env dt)."""
+    h = spec.bdt / spec.tau
     J = int(round(spec.pc_length / h)) + 1
     J = max(J, n_rows)
     s = np.arange(J, dtype=np.float64) * h
     a = spec.alpha
-    x = np.exp(-spec.alpha_phase * s)                      # exp phase at t = s*tau (+delay)
+    x = exp64(-spec.alpha_phase * s)                       # exp phase at t = s*tau (+delay)
     phi = rbf64(spec, x)                                   # [J, nb]
-    e = np.exp(a * s / 2)
+    e = exp64(a * s / 2)
     dp1 = (s * e * x)[:, None] * phi
     dp2 = (e * x)[:, None] * phi
     p1 = np.zeros_like(dp1)
@@ -139,7 +180,7 @@ def prodmp_fine64(spec, n_rows):
     for j in range(1, J):                                  # cumulative trapezoid
         p1[j] = p1[j - 1] + h * (dp1[j - 1] + dp1[j]) / 2
         p2[j] = p2[j - 1] + h * (dp2[j - 1] + dp2[j]) / 2
-    y1 = np.exp(-a * s / 2)
+    y1 = exp64(-a * s / 2)
     y2 = s * y1
     dy1 = -a / 2 * y1
     dy2 = -a / 2 * y2 + y1
@@ -166,23 +207,25 @@ def build_tables(spec, n_rows):
         s32 = np.maximum((t - spec.delay) / spec.tau, 0.0).astype(f32)
         return dict(psi=psi, sdt=(s32[1:] - s32[:-1]).astype(f32))
     if spec.kind == "prodmp":
-        fine = prodmp_fine64(spec, n_rows)
-        if spec.delay:
+        if spec.delay or spec.bdt != spec.dt:   # row i = fine-grid row j(i)
             j = prodmp_delay_index(spec, t[:n_rows])
+            fine = prodmp_fine64(spec, int(j.max()) + 1)
             fine = {k: v[j] for k, v in fine.items()}
+        else:                                   # j(i) = i
+            fine = prodmp_fine64(spec, n_rows)
         return {k: v.astype(f32) for k, v in fine.items()}
     raise ValueError(spec.kind)
 
 
 def prodmp_delay_index(spec, t):
-    """ProDMP with a delay: fine-grid index of time t on the left-bounded linear phase,
-    rint(max((t - delay) / tau, 0) / (dt / tau)) — mp_pytorch's ProDMP basis looks its
-    precomputed rows up at the rounded scaled-time index of the (delay-shifted, clamped at 0)
+    """ProDMP with a delay or its own basis dt: fine-grid index of time t on the left-bounded
+    linear phase, rint(max((t - delay) / tau, 0) / (bdt / tau)) — mp_pytorch's ProDMP basis looks
+    its precomputed rows up at the rounded scaled-time index of the (delay-shifted, clamped at 0)
     linear phase.  Parity unpinned like the rest of this module; what the reference's tests pin
     for a ProDMP delay (constant position and velocity before the delay, moving after,
     test_black_box.py:267-307) is re-checked in tests/test_mp_structure.py."""
     u = np.maximum((np.asarray(t, np.float64) - spec.delay) / spec.tau, 0.0)
-    return np.rint(u / (spec.dt / spec.tau)).astype(np.int64)
+    return np.rint(u / (spec.bdt / spec.tau)).astype(np.int64)
 
 
 # ----------------------------------------------------------------------------- trajectories

@@ -42,12 +42,12 @@ def test_tables_and_trajectories(ci):
     assert spec.basis_outside == over["basis_generator_kwargs"]["num_basis_outside"]
     got = np_(env.tables())
     ref = oracle_tables(spec, got.shape[0])
-    assert ulp_diff32(got[:, :ref.shape[1]], ref).max() <= 1
+    assert ulp_diff32(got[:, :ref.shape[1]], ref).max() == 0   # bit-exact (csrc/fgx_exp.h)
     # the outside centres change the basis: tables differ from num_basis_outside = 0
     ref0 = oracle_tables(mp.replace(spec, basis_outside=0), got.shape[0])
     assert not np.array_equal(ref, ref0)
     env.reset(seed=3)
-    tabs = split_tables(spec, got)
+    tabs = mp.build_tables(spec, got.shape[0])   # the oracle's own tables
     params = np.random.default_rng(ci).standard_normal((N, env.n_params), dtype=np.float32)
     st = env.get_state()
     pos, vel = env.trajectory(torch.from_numpy(params).to(DEV))
@@ -63,7 +63,7 @@ def test_bb_step_vs_oracle(ci):
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
     spec = spec_of(env)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec,
-                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+                           **oracle_kwargs(env))
     close(np_(env.reset(seed=9)[0]), ob.reset(seed=9))
     rng = np.random.default_rng(100 + ci)
     for _ in range(2):

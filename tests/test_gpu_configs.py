@@ -47,7 +47,7 @@ def params_seq(N, P, n_bb):
 
 def subset_oracle(env, name, idx, params, over_kw):
     spec = spec_of(env)
-    ob = batched.BatchedBB(name, len(idx), ctrl_of(env), mp_spec=spec, tables=split_tables(spec, np_(env.tables())),
+    ob = batched.BatchedBB(name, len(idx), ctrl_of(env), mp_spec=spec,
                            **over_kw)
     o0 = ob._reset_idx(list(range(len(idx))), [int(i) for i in idx])
     return ob, o0
@@ -98,7 +98,7 @@ def test_config3_full_batch_flags_and_lengths():
         _, ret, te, tr, info = env.step(torch.from_numpy(p).to(DEV))
         got.append((np_(info["trajectory_length"]), np_(te).astype(bool), np_(tr).astype(bool), np_(ret)))
     spec = spec_of(env)
-    tables = split_tables(spec, np_(env.tables()))
+    tables = None   # each worker's oracle builds its own tables (bit-identical to the device's)
     chunks = 16
     step = N // chunks
     jobs = [("HoleReacher", ctrl_of(env), spec, tables, oracle_kwargs(env), lo, lo + step,

@@ -9,7 +9,7 @@ import torch
 import fancy_gym_crowd_amd as fgx
 from oracle import batched
 
-from test_gpu_parity import DEV, kernel_is, NAME, assert_ulps, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables
+from test_gpu_parity import DEV, kernel_is, NAME, assert_ulps, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables, oracle_tables_dict
 
 pytestmark = pytest.mark.gpu
 
@@ -28,7 +28,7 @@ def test_single_env_vs_oracle(env_id, kern, monkeypatch):
     env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
     assert kernel_is(env.episode_kernel(), "k_episode_jl" if kern == "jl" else "k_episode")
     spec = spec_of(env)
-    tabs = split_tables(spec, np_(env.tables()))
+    tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, tables=tabs,
                            **oracle_kwargs(env))
     close(np_(env.reset(seed=5)[0]), ob.reset(seed=5))

@@ -12,7 +12,7 @@ import torch
 
 import fancy_gym_crowd_amd as fgx
 from oracle import batched
-from test_gpu_parity import NAME, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables
+from test_gpu_parity import NAME, close, ctrl_of, np_, oracle_kwargs, spec_of, split_tables, oracle_tables_dict
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -45,7 +45,7 @@ def test_info_rows_vs_oracle(ci, N):
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
     assert env.episode_kernel(info_level=2) == "k_episode"
     spec = spec_of(env)
-    tabs = split_tables(spec, np_(env.tables()))
+    tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=2, tables=tabs,
                            **oracle_kwargs(env))
     env.reset(seed=500)

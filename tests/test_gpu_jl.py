@@ -75,7 +75,7 @@ def test_jl_vs_oracle_desynchronised():
         assert kernel_is(env.episode_kernel(), "k_episode_jl")
         spec = spec_of(env)
         ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
-                               tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+                               **oracle_kwargs(env))
         env.reset(seed=23)
         ob.reset(seed=23)
         steps = (np.arange(N) % 200).astype(np.int32)

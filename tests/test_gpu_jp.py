@@ -118,7 +118,7 @@ def test_jp_vs_oracle_desynchronised():
     env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
     spec = spec_of(env)
     ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
-                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+                           **oracle_kwargs(env))
     env.reset(seed=21)
     ob.reset(seed=21)
     steps = (np.arange(N) % 200).astype(np.int32)

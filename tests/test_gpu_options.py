@@ -164,7 +164,7 @@ def test_default_info_level_is_verbose2():
 def _run_vs_oracle(env, name, params_list, setup=None, n_exact_frac=0.0):
     N = env.num_envs
     spec = spec_of(env)
-    ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec, tables=split_tables(spec, np_(env.tables())),
+    ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec,
                            **oracle_kwargs(env))
     close(np_(env.reset(seed=300)[0]), ob.reset(seed=300))
     if setup is not None:

@@ -70,6 +70,12 @@ def oracle_tables(spec, rows):
     return np.concatenate([t[key], t[last][:rows, None]], 1)
 
 
+def oracle_tables_dict(spec, env):
+    """The oracle's own tables (oracle/mp.py:build_tables) over the handle's row count: what every
+    device-vs-oracle comparison uses (test_tables_bit_exact pins them equal to the device's)."""
+    return mp.build_tables(spec, env._eng.dims.table_rows)
+
+
 def split_tables(spec, arr):
     nb = spec.n_basis
     if spec.kind == "prodmp":
@@ -140,15 +146,16 @@ MP_IDS = ["fancy_ProMP/LongSimpleReacher-v0", "fancy_ProMP/SimpleReacher-v0", "f
 
 
 @pytest.mark.parametrize("env_id", MP_IDS)
-def test_tables_within_one_ulp(env_id):
+def test_tables_bit_exact(env_id):
+    """The device's basis tables equal the oracle's (oracle/mp.py:build_tables) bit for bit: both
+    compute in f64 with the same exp (csrc/fgx_exp.h == oracle/mp.py:exp64) and round once to f32."""
     env = fgx.make(env_id, num_envs=8, device=DEV)
     spec = spec_of(env)
     got = np_(env.tables())
     ref = oracle_tables(spec, got.shape[0])
     got = got[:, :ref.shape[1]]
     d = ulp_diff32(got, ref)
-    assert d.max() <= 1, f"max ulp diff {d.max()}"
-    assert (d == 0).mean() > 0.99
+    assert d.max() == 0, f"{int((d != 0).sum())} entries differ, max {d.max()} ulp"
 
 
 @pytest.mark.parametrize("env_id", MP_IDS)
@@ -157,7 +164,7 @@ def test_trajectory_bit_exact(env_id):
     env = fgx.make(env_id, num_envs=N, device=DEV)
     env.reset(seed=11)
     spec = spec_of(env)
-    tabs = split_tables(spec, np_(env.tables()))
+    tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     rng = np.random.default_rng(0)
     params = rng.standard_normal((N, env.n_params), dtype=np.float32)
     st = env.get_state()
@@ -232,7 +239,7 @@ def test_bb_step_vs_oracle(ci):
     env_id, over, N, n_bb = FULL[ci]
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
     spec = spec_of(env)
-    tabs = split_tables(spec, np_(env.tables()))
+    tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     name = NAME[env_id.split("/")[1]]
     ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec, info_level=2, tables=tabs, **oracle_kwargs(env))
     o_g, _ = env.reset(seed=1000)
@@ -315,7 +322,7 @@ def test_bb_fast_path_vs_oracle(ci, monkeypatch):
     spec = spec_of(env)
     name = NAME[env_id.split("/")[1]]
     ob = batched.BatchedBB(name, N, ctrl_of(env), mp_spec=spec, info_level=0,
-                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+                           **oracle_kwargs(env))
     close(np_(env.reset(seed=2000)[0]), ob.reset(seed=2000))
     rng = np.random.default_rng(91)
     n_exact = 0
@@ -383,7 +390,7 @@ def test_large_batch_invariants():
     idx = np.arange(0, N, N // 64)
     spec = spec_of(env)
     ob = batched.BatchedBB("LongSimpleReacher", len(idx), ctrl_of(env), mp_spec=spec,
-                           tables=split_tables(spec, np_(env.tables())))
+                           )
     ob._reset_idx(list(range(len(idx))), [int(i) for i in idx])
     _, r_ret, _, _, r_info = ob.step(np_(params)[idx])
     close(np_(ret)[idx], r_ret)
@@ -423,7 +430,7 @@ def test_per_joint_pd_gains():
     env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     spec = spec_of(env)
     ob = batched.BatchedBB("LongSimpleReacher", N, ctrl_of(env), mp_spec=spec,
-                           tables=split_tables(spec, np_(env.tables())), **oracle_kwargs(env))
+                           **oracle_kwargs(env))
     assert ctrl_of(env)[1].shape == (5,)
     close(np_(env.reset(seed=8)[0]), ob.reset(seed=8))
     rng = np.random.default_rng(1)
@@ -446,7 +453,7 @@ def test_generic_basis_count(ci):
     env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
     spec = spec_of(env)
     assert spec.n_basis == nb and env.n_params == spec.n_params
-    tabs = split_tables(spec, np_(env.tables()))
+    tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     ref_t = oracle_tables(spec, np_(env.tables()).shape[0])
     assert ulp_diff32(np_(env.tables())[:, :ref_t.shape[1]], ref_t).max() <= 1
     env.reset(seed=4)
@@ -546,7 +553,7 @@ def test_set_state_then_step_matches_oracle():
     np.testing.assert_array_equal(back["qd"], qd)
     np.testing.assert_array_equal(back["steps"], steps)
     spec = spec_of(env)
-    ob = batched.BatchedBB("HoleReacher", N, ctrl_of(env), mp_spec=spec, tables=split_tables(spec, np_(env.tables())),
+    ob = batched.BatchedBB("HoleReacher", N, ctrl_of(env), mp_spec=spec,
                            **oracle_kwargs(env))
     ob.reset(seed=17)
     ob.env.q, ob.env.qd, ob.env.steps = q.copy(), qd.copy(), steps.astype(np.int64)

@@ -117,7 +117,7 @@ def test_bb_step_vs_oracle(ci, info_level):
     env = fgx.make(env_id, num_envs=N, device=DEV, info_level=info_level, **kw)
     spec = spec_of(env)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=info_level,
-                           tables=split_tables(spec, np_(env.tables())), env_kwargs=kw, **oracle_kwargs(env))
+                           env_kwargs=kw, **oracle_kwargs(env))
     close(np_(env.reset(seed=300)[0]), ob.reset(seed=300))
     rng = np.random.default_rng(8)
     for b in range(n_bb):
@@ -165,7 +165,7 @@ def test_replanning_schedule_program(ci, info_level):
     okw = oracle_kwargs(env)
     okw.pop("replan_period")
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=info_level,
-                           tables=split_tables(spec, np_(env.tables())), env_kwargs=kw, schedule=sched, **okw)
+                           env_kwargs=kw, schedule=sched, **okw)
     close(np_(env.reset(seed=600)[0]), ob.reset(seed=600))
     rng = np.random.default_rng(9)
     lens = set()

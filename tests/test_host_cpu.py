@@ -57,8 +57,9 @@ def test_library_loads_and_reports_abi():
 def test_config_struct_layout_matches_header():
     # 20 int32, 18 doubles, (ABI 2) 4 int32 and 8 doubles, (ABI 3) 17 int32 + pad and 8 doubles,
     # (ABI 4) 2 int32 and 16 doubles, (ABI 6) 4 int32 and 21 doubles
+    # (ABI 8) + basis_dt
     assert ctypes.sizeof(_lib.FgxConfig) == (20 * 4 + 18 * 8 + 4 * 4 + 8 * 8 + 17 * 4 + 4 + 8 * 8 + 2 * 4 + 16 * 8
-                                             + 4 * 4 + 21 * 8)
+                                             + 4 * 4 + 21 * 8 + 8)
     assert ctypes.sizeof(_lib.FgxInfo) == 11 * 8
 
 
@@ -249,3 +250,62 @@ def test_oracle_centres_with_basis_outside():
         np.testing.assert_allclose(c, u if phase == "linear" else np.exp(-3.0 * u), rtol=1e-15)
         c0, _ = mp.centers64(mp.replace(s, basis_outside=0))
         np.testing.assert_array_equal(c0, mp.centers64(mp.MPSpec("dmp", 2, 7, phase, 2.0, alpha_phase=3.0))[0])
+
+
+def test_table_exp_restatement_is_bit_exact(tmp_path):
+    """csrc/fgx_exp.h (the basis tables' exp) compiled for the host equals oracle/mp.py:exp64 bit for
+    bit: the same IEEE operations in the same order (no fma on either side)."""
+    from oracle import mp
+    src = tmp_path / "e.cpp"
+    src.write_text('#include "fgx_exp.h"\n'
+                   'extern "C" void run(const double* x, double* y, long n) {\n'
+                   '  for (long i = 0; i < n; ++i) y[i] = fgx::fgx_exp(x[i]);\n}\n')
+    so = tmp_path / "libe.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-D__host__=", "-D__device__=", "-shared", "-fPIC",
+                    "-I", os.path.join(ROOT, "fancy_gym_crowd_amd", "csrc"), str(src), "-o", str(so)], check=True)
+    lib = ctypes.CDLL(str(so))
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-760, 720, 400000), rng.uniform(-40, 40, 400000), rng.uniform(-1, 1, 100000),
+                        [0.0, -0.0, np.inf, -np.inf, np.nan, 709.78, 709.79, 709.8, -745.1, -745.2, -746.0, -708.4,
+                         -700.0, -1e-300, 5e-324]])
+    y = np.empty_like(x)
+    lib.run(x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p), ctypes.c_long(x.size))
+    ref = mp.exp64(x)
+    np.testing.assert_array_equal(y.view(np.int64), ref.view(np.int64))
+    fin = np.isfinite(ref) & (ref > 1e-300)
+    with np.errstate(over="ignore"):
+        assert (np.abs(ref[fin] - np.exp(x[fin])) <= np.spacing(np.exp(x[fin]))).all()   # within 1 ulp of numpy
+
+
+def test_link_counts_resolve():
+    """n_links 1..8 (base_reacher.py:17-39 takes any count; bb_env_constructor forwards env kwargs,
+    envs/registry.py:280-281); outside the engine's range a ValueError."""
+    for n in range(1, 9):
+        c, meta = fgx.resolve("fancy_ProMP/SimpleReacher-v0", n_links=n)
+        assert c.n_links == n and meta["n_params"] == 5 * n
+        c, meta = fgx.resolve("fancy_ProDMP/ViaPointReacher-v0", n_links=n)
+        assert meta["n_params"] == 6 * n
+    with pytest.raises(ValueError):
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", n_links=9)
+    with pytest.raises(IndexError):   # the reference's wall check cannot index one squeezed link
+        fgx.resolve("fancy_ProMP/HoleReacher-v0", n_links=1)
+    c, _ = fgx.resolve("fancy_ProMP/HoleReacher-v0", n_links=1, allow_wall_collision=True)
+    assert c.n_links == 1 and c.allow_wall_collision == 1
+
+
+def test_prodmp_basis_dt_resolution():
+    """basis_generator_kwargs dt (basis_generator_factory.py:8-23 forwards it to the ProDMP generator)."""
+    c, _ = fgx.resolve("fancy_ProDMP/SimpleReacher-v0")
+    assert c.basis_dt == c.dt == 0.01
+    c, _ = fgx.resolve("fancy_ProDMP/HoleReacher-v0", {"basis_generator_kwargs": {"dt": 0.005}})
+    assert c.basis_dt == 0.005
+    with pytest.raises(TypeError):   # the RBF generators take no dt
+        fgx.resolve("fancy_ProMP/SimpleReacher-v0", {"basis_generator_kwargs": {"dt": 0.005}})
+    from oracle import mp
+    # the oracle's row map: rint(t_i / bdt) on the fine grid (j(i) = 2 i for bdt = dt / 2)
+    s = mp.MPSpec("prodmp", 2, 5, "exp", 1.5, alpha=10.0, basis_dt=0.005)
+    j = mp.prodmp_delay_index(s, np.arange(50) * 0.01)
+    np.testing.assert_array_equal(j, 2 * np.arange(50))
+    t = mp.build_tables(s, 50)
+    f = mp.prodmp_fine64(s, 99)
+    np.testing.assert_array_equal(t["pb"], f["pb"][::2].astype(np.float32))
