@@ -766,12 +766,25 @@ struct Env {
       auto lin = [](int j) { return j == 99 ? 1.0 : (double)j * (1.0 / 99.0); };
       auto px = [&](int j) { return ck * lin(j) + bx; };
       auto py = [&](int j) { return sk * lin(j) + by; };
-      // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none: the estimate je
-      // (the real-valued crossing, rounded up) is checked with two evaluations of the very same point
-      // expressions -- pred(je - 1) false and pred(je) true -- and only a lane whose estimate misses
-      // (a crossing within rounding of a point, NaN / inf state) runs the 7-step binary search
-      auto first = [&](auto pred, float est) {
+      // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none.  The estimate je
+      // (the real-valued crossing, rounded up) is exact without evaluating a point when the crossing
+      // is far from every index (`clear`, below); otherwise it is checked with two evaluations of the
+      // very same point expressions -- pred(je - 1) false and pred(je) true -- and only a lane whose
+      // estimate misses (a crossing within rounding of a point, NaN / inf state) runs the 7-step
+      // binary search.
+      // Why `clear` is exact: the evaluated point f(j) = fl(fl(k lin_j) + b) differs from the real
+      // F(j) = k j / 99 + b by at most E = 4u (|k| + |b|) (u = 2^-53; lin_j within 2u of j / 99), so
+      // the comparison of f(j) with t is decided by the side of j against the real crossing
+      // j* = 99 (t - b) / k whenever |j - j*| > 99 E / |k| <= 5e-8 (|k| >= 1e-3, |b|, |t| <= 1e3:
+      // `sane`).  est = fl32(fl32(t - b) * fl32(rcp32(fl32(k)) * 99)) is within 6 f32 roundings of j*
+      // (relative 5e-7, rcp32 1 ulp): |est - j*| < 6e-5 for |est| <= 101.  So when est lies more than
+      // 1e-4 from every integer, or beyond [-1, 101], ceil(est) clamped to [0, 100] is the index the
+      // binary search would find.
+      auto first = [&](auto pred, float est, bool sane) {
         const int je = (est > 0.0f) ? ((est < 100.0f) ? (int)__builtin_ceilf(est) : 100) : 0;
+        const float fr = est - __builtin_floorf(est);
+        const bool clear = sane && (est < -1.0f || est > 101.0f || (fr > 1e-4f && fr < 1.0f - 1e-4f));
+        if (__builtin_expect(clear, 1)) return je;
         const bool ok = (je == 0 || !pred(je - 1)) && (je == 100 || pred(je));
         if (__builtin_expect(ok, 1)) return je;
         int lo = 0, hi = 100;
@@ -786,25 +799,29 @@ struct Env {
       // real-valued index where f(j) = b + k j / 99 crosses t (an estimate only)
       const float rck = __builtin_amdgcn_rcpf((float)ck) * 99.0f, rsk = __builtin_amdgcn_rcpf((float)sk) * 99.0f;
       auto cross = [](double t, double b, float r) { return (float)(t - b) * r; };
+      // the bounds under which an estimate far from every index is exact (`first`)
+      const bool tsane = __builtin_fabs(left) <= 1e3 && __builtin_fabs(right) <= 1e3 && __builtin_fabs(nd) <= 1e3;
+      const bool xsane = tsane && __builtin_fabs(ck) >= 1e-3 && __builtin_fabs(bx) <= 1e3;
+      const bool ysane = tsane && __builtin_fabs(sk) >= 1e-3 && __builtin_fabs(by) <= 1e3;
       // {j : f(j) < t} / {j : f(j) > t} as [lo, hi) for f monotone with slope sign of `dir`
-      auto below = [&](auto f, double dir, double t, float est, int& lo, int& hi) {
-        if (dir > 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) < t); }, est); }
-        else if (dir < 0.0) { lo = first([&](int j) { return f(j) < t; }, est); hi = 100; }
+      auto below = [&](auto f, double dir, double t, float est, bool sane, int& lo, int& hi) {
+        if (dir > 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) < t); }, est, sane); }
+        else if (dir < 0.0) { lo = first([&](int j) { return f(j) < t; }, est, sane); hi = 100; }
         else { lo = 0; hi = (f(0) < t) ? 100 : 0; }   // constant (or NaN) along the link
       };
-      auto above = [&](auto f, double dir, double t, float est, int& lo, int& hi) {
-        if (dir > 0.0) { lo = first([&](int j) { return f(j) > t; }, est); hi = 100; }
-        else if (dir < 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) > t); }, est); }
+      auto above = [&](auto f, double dir, double t, float est, bool sane, int& lo, int& hi) {
+        if (dir > 0.0) { lo = first([&](int j) { return f(j) > t; }, est, sane); hi = 100; }
+        else if (dir < 0.0) { lo = 0; hi = first([&](int j) { return !(f(j) > t); }, est, sane); }
         else { lo = 0; hi = (f(0) > t) ? 100 : 0; }
       };
       int xl0, xl1, xr0, xr1, xL0, xL1, xR0, xR1, yg0, yg1, yd0, yd1;
       const float el = cross(left, bx, rck), er = cross(right, bx, rck);
-      below(px, ck, left, el, xl0, xl1);    // px < left
-      above(px, ck, right, er, xr0, xr1);   // px > right
-      above(px, ck, left, el, xL0, xL1);    // px > left
-      below(px, ck, right, er, xR0, xR1);   // px < right
-      below(py, sk, 0.0, cross(0.0, by, rsk), yg0, yg1);   // py < 0
-      below(py, sk, nd, cross(nd, by, rsk), yd0, yd1);     // py < -depth
+      below(px, ck, left, el, xsane, xl0, xl1);    // px < left
+      above(px, ck, right, er, xsane, xr0, xr1);   // px > right
+      above(px, ck, left, el, xsane, xL0, xL1);    // px > left
+      below(px, ck, right, er, xsane, xR0, xR1);   // px < right
+      below(py, sk, 0.0, cross(0.0, by, rsk), ysane, yg0, yg1);   // py < 0
+      below(py, sk, nd, cross(nd, by, rsk), ysane, yd0, yd1);     // py < -depth
       const bool c1 = max(xl0, yg0) < min(xl1, yg1);
       const bool c2 = max(xr0, yg0) < min(xr1, yg1);
       const bool c3 = max(max(xL0, xR0), yd0) < min(min(xL1, xR1), yd1);

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "fgx_ws.h"
+#include "fgx_v2.h"
 
 // returns 0 / FGX_E_* code, message in err
 #define FGX_DECLARE_LAUNCH(NAME)                                                                             \
@@ -68,7 +69,7 @@ namespace fgx {
 //    its exchange rows stopped conflicting on LDS banks).
 // k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
 // wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_PAIR = 5 };
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_PAIR = 5, EK_V2 = 6 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -106,7 +107,21 @@ inline int classic_choice(const DevCfg& c, bool log) {
   return c.N > round_envs() ? EK_CLASSIC_W2 : EK_CLASSIC;
 }
 
+// k_episode_v2 (fgx_v2.h): the per-step info arrays of SimpleReacher + PD (info_level >= 1, the
+// reference's verbose-2 default) with the observation's trigonometry on a second wave of each SIMD;
+// FGX_V2=0 (or FGX_EPISODE_KERNEL=classic) keeps the logging k_episode (A/B, tests)
+inline bool v2_applies(const DevCfg& c, int mp, bool log, bool per_env_plans) {
+  if (const char* v = std::getenv("FGX_V2"))
+    if (std::strcmp(v, "0") == 0) return false;
+  if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))   // a forced kernel wins
+    if (std::strcmp(v, "classic") == 0) return false;
+  return log && c.env == ENV_SIMPLE && c.ctrl == CTRL_PD && mp != MP_GIVEN && mp != MP_NONE && !per_env_plans &&
+         !c.learn_tau && !c.learn_delay && !c.sched_state && c.valid_flags == 0 && c.T <= 256 && c.max_steps <= 200 &&
+         (c.nl == 2 || c.nl == 5) && v2_lds_bytes(c.rows, c.stride, c.nl) <= 160 * 1024;
+}
+
 inline int episode_kernel_choice(const DevCfg& c, int mp, bool log, bool per_env_plans) {
+  if (v2_applies(c, mp, log, per_env_plans)) return EK_V2;
   const bool eligible = c.env == ENV_SIMPLE && mp != MP_GIVEN && mp != MP_NONE && c.ctrl == CTRL_PD && !log &&
                         !c.sched_state && c.T <= 256 && c.max_steps <= 200 && !per_env_plans && !c.learn_tau &&
                         !c.learn_delay && (c.nl == 2 || c.nl == 5);
@@ -187,6 +202,19 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
   }
   if constexpr (!LOG_ONLY && ENV == ENV_SIMPLE && MP != MP_GIVEN && CTRL == CTRL_PD) {
     const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
+    if (k == EK_V2) {
+      const size_t lv = v2_lds_bytes(c.rows, c.stride, NL);
+      if (lv > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_v2<MP, NL, NB>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv) != hipSuccess) {
+        err = "k_episode_v2: cannot raise the dynamic LDS limit";
+        return -2;
+      }
+      hipLaunchKernelGGL((k_episode_v2<MP, NL, NB>), dim3((unsigned)((c.N + 64 * kV2Pairs - 1) / (64 * kV2Pairs))),
+                         dim3(128 * kV2Pairs), lv, stream, c, s, params, o);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) { err = std::string("k_episode_v2 launch: ") + hipGetErrorString(e); return -2; }
+      return 0;
+    }
     if (k == EK_JP) return launch_jp<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_WS) return launch_ws<MP, NL, NB>(c, s, params, o, stream, err);
     if (k == EK_JL) return fgx_launch_episode_jl(c, s, MP, NB, params, o, stream, err);

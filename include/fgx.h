@@ -266,10 +266,11 @@ int fgx_get_tables(void* handle, float* out, void* stream);
  * arrays): 0 = k_episode (one env per lane), 1 = k_episode_jp (one wave per joint),
  * 2 = k_episode_ws (trajectory producer / dynamics consumer wave pairs), 3 = k_episode_jl (one lane
  * per env x joint), 4 = k_episode_w2 (k_episode for two resident waves per SIMD), 5 = k_episode_pair
- * (HoleReacher, two lanes per env); negative on error.
+ * (HoleReacher, two lanes per env), 6 = k_episode_v2 (SimpleReacher + PD with per-step arrays: dynamics
+ * and observation-trigonometry waves side by side); negative on error.
  * info_level >= 1 means some per-step output pointer is given (the launch then runs the logging
- * k_episode, as it does for a config with valid_flags).  All six give bit-identical results; the
- * choice follows measured speed (fgx_dispatch.h). */
+ * k_episode or k_episode_v2, as it does for a config with valid_flags).  All seven give bit-identical
+ * results; the choice follows measured speed (fgx_dispatch.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 
 /* Diagnostics (tests): for x[0..n) (device f64), out[4 n] = {sin, cos} of the kernels' sincos

@@ -1,5 +1,6 @@
 """The verbose-2 per-step info arrays row by row (black_box_wrapper.py:184-189,218-227,244-249),
-written by the logging k_episode through the wave's LDS staging slots (InfoStage, fgx_device.h).
+written by the logging k_episode through the wave's LDS staging slots (InfoStage, fgx_device.h), and
+for SimpleReacher + PD by k_episode_v2 (fgx_v2.h: dynamics and observation-trigonometry waves).
 
 Every element of every array is checked, not only the rows before trajectory_length: rows < L
 against the oracle, rows >= L as the host contract states (NaN; 0 for the flags), the desired plan
@@ -43,7 +44,8 @@ def _rows(dev, ref, L, name, T):
 def test_info_rows_vs_oracle(ci, N):
     env_id, over = CASES[ci]
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
-    assert env.episode_kernel(info_level=2) == "k_episode"
+    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher: the logging k_episode
+    assert env.episode_kernel(info_level=2) == ("k_episode" if "Hole" in env_id else "k_episode_v2")
     spec = spec_of(env)
     tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=2, tables=tabs,
@@ -96,3 +98,46 @@ def test_logging_step_equals_fast_step(env_id, over):
             so = np_(ia["step_observations"])
             last = so[np.arange(N), L - 1]
             np.testing.assert_array_equal(last, np_(ia["final_observation"]))
+
+
+V2_CASES = [
+    ("fancy_ProMP/LongSimpleReacher-v0", None, {}),
+    ("fancy_DMP/LongSimpleReacher-v0", None, {}),
+    ("fancy_ProDMP/SimpleReacher-v0", REPLAN, {}),
+    ("fancy_ProMP/SimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(30),
+                                                           "condition_on_desired": True}}, {}),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"basis_generator_kwargs": {"num_basis": 7}}, {}),   # generic basis count
+    ("fancy_ProMP/SimpleReacher-v0", None, {"target": (0.5, 1.0)}),
+]
+
+
+@pytest.mark.parametrize("N", [1000, 203])
+@pytest.mark.parametrize("info_level", [1, 2])
+@pytest.mark.parametrize("ci", range(len(V2_CASES)))
+def test_v2_equals_logging_kernel(ci, info_level, N, monkeypatch):
+    """k_episode_v2 (fgx_v2.h) against the logging k_episode + k_info_obs (FGX_V2=0, read at every
+    launch): every per-step array, the step outputs and the whole device state bit for bit (NaN
+    padding included), over steps that truncate and auto-reset (6 BB steps of up to 200 samples,
+    TimeLimit 200), partial last waves (203, 1000) and replanning segments."""
+    env_id, over, kw = V2_CASES[ci]
+    a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    assert a.episode_kernel() == "k_episode_v2"
+    np.testing.assert_array_equal(np_(a.reset(seed=8)[0]), np_(b.reset(seed=8)[0]))
+    rng = np.random.default_rng(ci + 10 * info_level)
+    for _ in range(6):
+        p = torch.from_numpy((rng.standard_normal((N, a.n_params)) * 3).astype(np.float32)).to(DEV)
+        monkeypatch.delenv("FGX_V2", raising=False)
+        ra = a.step(p)
+        monkeypatch.setenv("FGX_V2", "0")
+        rb = b.step(p)
+        monkeypatch.delenv("FGX_V2")
+        for x, y in zip(ra[:4], rb[:4]):
+            np.testing.assert_array_equal(np_(x), np_(y))
+        keys = [k for k in ra[4] if isinstance(ra[4][k], torch.Tensor) and not k.startswith("_")]
+        assert "reward_dist" in keys and (info_level < 2 or "step_observations" in keys)
+        for k in keys:
+            np.testing.assert_array_equal(np_(ra[4][k]), np_(rb[4][k]), err_msg=k)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)

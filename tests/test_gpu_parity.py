@@ -603,16 +603,21 @@ def test_step_before_reset_raises():
 
 @pytest.mark.parametrize("env_id,N", [("fancy_ProMP/LongSimpleReacher-v0", 4099), ("fancy_ProDMP/HoleReacher-v0", 4099),
                                       ("fancy_ProMP/SimpleReacher-v0", 1000), ("fancy_ProDMP/SimpleReacher-v0", 65536)])
-def test_trajectory_mfma_equals_valu(env_id, N):
-    """k_traj_mfma (one contiguous [envs, T, dof] output region per wave, MFMA columns = (env, joint)
-    pairs) against k_traj_valu on the same plans (a replanning schedule that never fires before T
-    routes get_trajectory to the VALU kernel): bit for bit, partial last wave included."""
+def test_trajectory_mfma_equals_valu(env_id, N, monkeypatch):
+    """k_traj_mfma (csrc/fgx_mfma.h: ProMP positions once, forward differences across the half-waves,
+    8-row LDS groups) against k_traj_valu on the same plans (a replanning schedule that never fires
+    before T routes get_trajectory to the VALU kernel) and against round 3's k_traj_mfma_r3
+    (FGX_TRAJ_R3): bit for bit, partial last wave included."""
     outs = []
-    for over in (None, {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}):
+    for over, r3 in ((None, False), ({"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}, False),
+                     (None, True)):
+        if r3:
+            monkeypatch.setenv("FGX_TRAJ_R3", "1")
         env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
         params = torch.from_numpy(np.random.default_rng(5).standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)
         env.reset(seed=3)
         outs.append([np_(x) for x in env.trajectory(params)])
-    for a, b in zip(outs[0], outs[1]):
-        assert a.shape == b.shape
-        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    for other in (outs[1], outs[2]):
+        for a, b in zip(outs[0], other):
+            assert a.shape == b.shape
+            np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -38,7 +38,7 @@ def test_w2_dispatch_past_one_round(monkeypatch):
     n_round = 4 * 64 * torch.cuda.get_device_properties(DEV).multi_processor_count
     env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=2 * n_round, device=DEV, info_level=0)
     assert env.episode_kernel() == "k_episode_w2"
-    assert env.episode_kernel(info_level=2) == "k_episode"
+    assert env.episode_kernel(info_level=2) == "k_episode_v2"   # per-step arrays: fgx_v2.h
     env1 = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=n_round, device=DEV, info_level=0)
     assert env1.episode_kernel() == "k_episode"
     # full-size run vs the forced k_episode on a strided subset of outputs

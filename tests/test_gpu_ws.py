@@ -55,7 +55,7 @@ def test_episode_kernel_selection():
     """fgx_episode_kernel reports the measured choice (fgx_dispatch.h episode_kernel_choice)."""
     rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
     cases = [("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 0, "k_episode"),      # the metric config
-             ("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode"),      # per-step info arrays
+             ("fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode_v2"),   # per-step info arrays
              ("fancy_ProMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),   # metric shards
              ("fancy_ProMP/LongSimpleReacher-v0", None, 8192, 0, "k_episode_jl"),
              ("fancy_ProMP/LongSimpleReacher-v0", None, 98304, 0, "k_episode_jl"),   # half-full 2nd round

@@ -17,3 +17,9 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 echo "bench rc=$?"
 cat gpurun_out/${TAG}_bench.json | cut -c1-600
+# optional: per-kernel timings (tools/bench_kernels.py modes, e.g. "episode hole")
+if [ -n "$3" ]; then
+  timeout -k 10 400 python tools/bench_kernels.py $3 > gpurun_out/${TAG}_kernels.jsonl 2> gpurun_out/${TAG}_kernels.err
+  echo "kernels rc=$?"
+  cut -c1-300 gpurun_out/${TAG}_kernels.jsonl
+fi
