@@ -570,11 +570,19 @@ static bool info_too_large(const Handle* h, const fgx_info* info) {
 
 // info_level 2 (per-step observations) on SimpleReacher: the logging k_episode logs q per sample and
 // k_info_obs derives the trigonometric observation components from it (fgx_kernels.h); the handle's
-// scratch for that is allocated on the first such step (T * n_links * N + 2 N doubles)
-static int attach_obs_scratch(Handle* h, Outputs& o) {
+// scratch for that is allocated on the first such step that needs it (T * n_links * N + 2 N doubles;
+// k_episode_v2 needs none).  A first such step inside a HIP graph capture is refused rather than
+// allocating there (hipMalloc would invalidate the capture): run it once before capturing.  Per-step
+// observations on one handle must stay on one stream (the scratch is per handle).
+static int attach_obs_scratch(Handle* h, Outputs& o, int mp, hipStream_t stream) {
   if (!o.step_obs || h->dc.env != ENV_SIMPLE) return FGX_OK;
+  if (episode_kernel_choice(h->dc, mp, true, h->learned()) == EK_V2) return FGX_OK;
   const size_t nq = (size_t)h->dc.T * h->dc.nl * h->dc.N;
   if (!h->obs_scratch) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(FGX_E_INVALID, "the first step with per-step observations allocates its scratch: "
+                                 "run it once outside the HIP graph capture");
     const hipError_t e = hipMalloc(&h->obs_scratch, sizeof(double) * (nq + 2 * (size_t)h->dc.N));
     if (e != hipSuccess) {
       h->obs_scratch = nullptr;
@@ -600,7 +608,7 @@ int fgx_step(void* handle, const float* params, float* obs, double* ret, uint8_t
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
-  if (const int rc = attach_obs_scratch(h, o)) return rc;
+  if (const int rc = attach_obs_scratch(h, o, h->learned() ? MP_GIVEN : h->dc.mp, (hipStream_t)stream)) return rc;
   if (h->learned()) {
     // per-env plans first (and, when requested, the time-major info copies), then the episode
     // over the given plans with per-env lengths
@@ -633,7 +641,7 @@ int fgx_step_traj(void* handle, const float* des_pos, const float* des_vel, floa
     return fail(FGX_E_INVALID, "reward_dist and reward_ctrl must be given together");
   if (info_too_large(h, info)) return fail(FGX_E_UNSUPPORTED, "per-step info arrays need n_envs < 2^24");
   Outputs o = make_outputs(obs, ret, terminated, truncated, traj_len, final_obs, info, autoreset);
-  if (const int rc = attach_obs_scratch(h, o)) return rc;
+  if (const int rc = attach_obs_scratch(h, o, MP_GIVEN, (hipStream_t)stream)) return rc;
   o.positions = nullptr;
   o.velocities = nullptr;   // the caller already holds the desired trajectories
   return launch_episode(*h, MP_GIVEN, nullptr, des_pos, des_vel, o, (hipStream_t)stream);

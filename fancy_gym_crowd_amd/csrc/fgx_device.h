@@ -766,6 +766,17 @@ struct Env {
       auto lin = [](int j) { return j == 99 ? 1.0 : (double)j * (1.0 / 99.0); };
       auto px = [&](int j) { return ck * lin(j) + bx; };
       auto py = [&](int j) { return sk * lin(j) + by; };
+      // a link that crosses no hole edge (x = left / right): px is monotone in j, so its points all lie
+      // on the side of both edges its end points p_0, p_99 lie on, and each condition reduces to the end
+      // points' y (py monotone too): c1 / c2 to "some py < 0", c3 to "some py < -depth" -- exact, no
+      // crossing search (needs left <= right; NaN end points fall through)
+      {
+        const double x0 = px(0), x1 = px(99), y0 = py(0), y1 = py(99);
+        if (left <= right) {
+          if ((x0 < left && x1 < left) || (x0 > right && x1 > right)) return y0 < 0.0 || y1 < 0.0;
+          if (x0 > left && x0 < right && x1 > left && x1 < right) return y0 < nd || y1 < nd;
+        }
+      }
       // first j in [0, 100) with pred(j) (pred monotone false -> true), 100 if none.  The estimate je
       // (the real-valued crossing, rounded up) is exact without evaluating a point when the crossing
       // is far from every index (`clear`, below); otherwise it is checked with two evaluations of the

@@ -62,6 +62,17 @@ class SingleEnv:
         self._env.close()
 
 
+def gym_spaces(env_id, gym_module, **env_kwargs):
+    """(observation_space, action_space) of one env of `env_id` as `gym_module.spaces.Box` instances
+    (same low / high / shape / dtype as the engine's own Box stand-in), from the resolved config
+    alone (no device work).  gymnasium's env checker requires spaces derived from gymnasium.spaces.Space."""
+    from .registry import resolve
+    from .vector_env import action_space, observation_space
+    cfg, meta = resolve(env_id, None, **env_kwargs)
+    conv = lambda b: gym_module.spaces.Box(low=b.low, high=b.high, shape=b.shape, dtype=b.dtype)   # noqa: E731
+    return conv(observation_space(cfg)), conv(action_space(cfg, meta.get("n_params", 0)))
+
+
 def registered_ids():
     from .registry import _BB_IDS, ENV_SPECS
     return sorted(ENV_SPECS) + sorted(_BB_IDS)
@@ -76,7 +87,12 @@ def register_gymnasium(device="cuda:0", gym_module=None):
             import gymnasium as gym
         except ImportError:
             return False
-    base = type("GymSingleEnv", (SingleEnv, gym.Env), {})
+    def _init(self, env_id, device="cuda:0", **kwargs):
+        SingleEnv.__init__(self, env_id, device, **kwargs)
+        # gymnasium's PassiveEnvChecker rejects spaces that are not gymnasium.spaces.Space instances
+        self.observation_space, self.action_space = gym_spaces(env_id, gym, **kwargs)
+
+    base = type("GymSingleEnv", (SingleEnv, gym.Env), {"__init__": _init})
     for env_id in registered_ids():
         # the engine keeps the registry's TimeLimit itself (the truncated flag), so gymnasium adds none
         gym.register(id=env_id, entry_point=functools.partial(base, env_id, device))

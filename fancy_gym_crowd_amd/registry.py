@@ -309,7 +309,14 @@ class TrajValidity:
     An invalid plan yields the artificial transition (no env step, trajectory_length 0):
     return ``invalid_return``, ``terminated`` / ``truncated`` as given (reference default: True /
     False), observation zeros (``obs='zeros'``, np.zeros) or the env's current one
-    (``obs='current'``).  ``__call__`` is the host predicate with the reference's signature."""
+    (``obs='current'``).  ``__call__`` is the host predicate with the reference's signature.
+
+    Comparison semantics follow numpy >= 2 (NEP 50), the numpy of this image: the raw float32 action
+    entry is compared with a Python-float bound in float32 (the bound rounded to f32 first); under
+    numpy 1.x value-based casting the same comparison ran in float64, so an action within one f32 ulp
+    of a bound that is not an f32 value can be classed differently there.  Pinned by
+    tests/test_host_cpu.py::test_validity_bound_semantics_follow_nep50 (host) and
+    tests/test_gpu_validity.py::test_tau_bound_one_ulp (device)."""
 
     def __init__(self, tau=None, delay=None, pos_low=None, pos_high=None, invalid_return=0.0,
                  terminated=True, truncated=False, obs='zeros'):

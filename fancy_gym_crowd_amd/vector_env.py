@@ -171,21 +171,7 @@ class BlackBoxVectorEnv:
         self._alloc()
 
     def _obs_space(self, cfg):
-        n = self.dof
-        extra = {_lib.ENV_SIMPLE: 0, _lib.ENV_HOLE: 1, _lib.ENV_VIA: 2}[cfg.env_kind]   # width | via - ee
-        bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf] * extra, [np.inf] * 2, [np.inf]])
-        low, high = -bound, bound
-        if cfg.time_aware:
-            low, high = np.append(low, 0.0), np.append(high, 1.0)
-        if cfg.return_context:
-            rs = [bool(cfg.random_start)] * (3 * n)
-            if cfg.env_kind == _lib.ENV_HOLE:
-                rs = rs + [math_isnan(cfg.hole_width)]
-            elif cfg.env_kind == _lib.ENV_VIA:
-                rs = rs + [math_isnan(cfg.via_x)] * 2
-            mask = rs + [True, True, False]
-            low, high = low[np.array(mask)], high[np.array(mask)]
-        return Box(low, high, dtype=np.float32)
+        return observation_space(cfg)
 
     def _alloc(self):
         N, dev = self.num_envs, self.device
@@ -429,6 +415,7 @@ class StepVectorEnv:
         self.device = self._eng.device
         bound = float(cfg.act_high)
         self.single_action_space = Box(-bound, bound, (self.dof,), np.float32)
+        self.single_observation_space = observation_space(cfg)
 
     def reset(self, *, seed=None, options=None):
         obs = torch.empty((self.num_envs, self.obs_dim), dtype=torch.float32, device=self.device)
@@ -524,3 +511,34 @@ def _reset_engine(env, seed, options, obs):
 
 def math_isnan(x):
     return x != x
+
+
+def observation_space(cfg):
+    """The observation Box of one env of a resolved config: the env's state bounds (base_reacher.py
+    observation_space: pi for cos / sin, inf otherwise), + TimeAwareObservation's [0, 1] entry
+    (utils/wrappers.py:49-63), context-masked for a black-box id (black_box_wrapper.py:90-95)."""
+    n = int(cfg.n_links)
+    extra = {_lib.ENV_SIMPLE: 0, _lib.ENV_HOLE: 1, _lib.ENV_VIA: 2}[cfg.env_kind]   # width | via - ee
+    bound = np.hstack([[np.pi] * n, [np.pi] * n, [np.inf] * n, [np.inf] * extra, [np.inf] * 2, [np.inf]])
+    low, high = -bound, bound
+    if cfg.time_aware:
+        low, high = np.append(low, 0.0), np.append(high, 1.0)
+    if cfg.return_context:
+        rs = [bool(cfg.random_start)] * (3 * n)
+        if cfg.env_kind == _lib.ENV_HOLE:
+            rs = rs + [math_isnan(cfg.hole_width)]
+        elif cfg.env_kind == _lib.ENV_VIA:
+            rs = rs + [math_isnan(cfg.via_x)] * 2
+        mask = rs + [True, True, False]
+        low, high = low[np.array(mask)], high[np.array(mask)]
+    return Box(low, high, dtype=np.float32)
+
+
+def action_space(cfg, n_params):
+    """The action Box of one env: the MP parameters (unbounded; learned tau / delay clipped inside the
+    step as the reference's get_trajectory does) or, for a step-based id, the env's torque / velocity
+    bounds in float32 (base_reacher_torque.py:16-18, base_reacher_direct.py:16-18)."""
+    if cfg.mp_kind != _lib.MP_NONE:
+        return Box(-np.inf, np.inf, (int(n_params),), np.float32)
+    bound = float(cfg.act_high)
+    return Box(-bound, bound, (int(cfg.n_links),), np.float32)

@@ -168,3 +168,24 @@ def test_device_median_at_metric_size_host_time():
     assert "step_rewards" not in info
     assert host < 0.05, host
     assert bool(torch.isfinite(ret).all())
+
+
+def test_tau_bound_one_ulp():
+    """The device classes a raw tau one f32 ulp around a bound that is not an f32 value exactly as the
+    host predicate does (numpy >= 2, NEP 50: compared in float32; registry.TrajValidity)."""
+    N = 64
+    val = fgx.TrajValidity(tau=(0.1, 0.3))
+    over = {"phase_generator_kwargs": {"learn_tau": True}}
+    env = fgx.make("fancy_ProMP/SimpleReacher-v0", num_envs=N, device=DEV, mp_config_override=over,
+                   traj_validity=val, info_level=0)
+    env.reset(seed=2)
+    p = np.zeros((N, env.n_params), np.float32)
+    at_hi, at_lo = np.float32(0.3), np.float32(0.1)
+    cand = [at_hi, np.nextafter(at_hi, np.float32(1)), np.nextafter(at_hi, np.float32(0)),
+            at_lo, np.nextafter(at_lo, np.float32(0)), np.nextafter(at_lo, np.float32(1))]
+    p[:, 0] = np.resize(np.array(cand, np.float32), N)
+    pos = np.zeros((env.T, env.dof), np.float32)
+    want = np.array([val(p[i], pos, pos)[0] for i in range(N)])
+    assert want.sum() == 4 * N // 6 or 0 < want.sum() < N
+    _, _, _, _, info = env.step(torch.from_numpy(p).to(DEV))
+    np.testing.assert_array_equal(np_(info["trajectory_length"]) > 0, want)

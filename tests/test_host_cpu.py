@@ -211,16 +211,41 @@ def test_per_joint_gains_resolution():
         fgx.resolve("fancy_ProMP/LongSimpleReacher-v0", {"controller_kwargs": {"p_gains": (1.0, 2.0)}})
 
 
+class _StandInSpaces:
+    """gymnasium.spaces stand-in: Space base class and Box(low, high, shape, dtype)."""
+
+    class Space:
+        pass
+
+    class Box(Space):
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.dtype = np.dtype(dtype)
+            self.shape = tuple(shape)
+            self.low = np.broadcast_to(np.asarray(low), self.shape).astype(self.dtype)
+            self.high = np.broadcast_to(np.asarray(high), self.shape).astype(self.dtype)
+
+
 def test_register_gymnasium_with_stand_in():
-    """envs/registry.py:245-254: every id reaches gym.make; without gymnasium nothing is registered."""
+    """envs/registry.py:245-254: every id reaches gym.make; without gymnasium nothing is registered.
+    The registered envs' spaces are gymnasium spaces (the PassiveEnvChecker's requirement)."""
     import types
+    from fancy_gym_crowd_amd import gym_compat
     calls = []
-    stand_in = types.SimpleNamespace(Env=object, register=lambda **kw: calls.append(kw))
+    stand_in = types.SimpleNamespace(Env=object, register=lambda **kw: calls.append(kw), spaces=_StandInSpaces)
     assert fgx.register_gymnasium(gym_module=stand_in) is True
     ids = [c["id"] for c in calls]
     assert "fancy_ProMP/LongSimpleReacher-v0" in ids and "fancy/HoleReacher-v0" in ids
     assert len(ids) == len(set(ids)) == 4 + 12
     assert all(callable(c["entry_point"]) for c in calls)
+    for env_id in ids:   # what GymSingleEnv.__init__ installs, for every id (step-based ones included)
+        obs, act = gym_compat.gym_spaces(env_id, stand_in)
+        assert isinstance(obs, _StandInSpaces.Space) and isinstance(act, _StandInSpaces.Space)
+        assert obs.dtype == np.float32 and act.dtype == np.float32
+    obs, act = gym_compat.gym_spaces("fancy_ProMP/LongSimpleReacher-v0", stand_in)
+    assert obs.shape == (17,) and act.shape == (25,)          # test_black_box.py:153-193 sizes
+    obs, act = gym_compat.gym_spaces("fancy/HoleReacher-v0", stand_in)
+    assert obs.shape == (19,) and act.shape == (5,)
+    assert act.high[0] == np.float32(2 * np.pi) and np.isinf(obs.high[-1])
     try:
         import gymnasium  # noqa: F401
     except ImportError:
@@ -309,3 +334,19 @@ def test_prodmp_basis_dt_resolution():
     t = mp.build_tables(s, 50)
     f = mp.prodmp_fine64(s, 99)
     np.testing.assert_array_equal(t["pb"], f["pb"][::2].astype(np.float32))
+
+
+def test_validity_bound_semantics_follow_nep50():
+    """TrajValidity compares the raw float32 action with a Python-float bound as numpy >= 2 does
+    (NEP 50: in float32).  0.3 is not an f32 value: f32(0.3) > 0.3 in float64, == in float32."""
+    assert int(np.__version__.split(".")[0]) >= 2
+    val = fgx.TrajValidity(tau=(0.1, 0.3))
+    pos = np.zeros((200, 2), np.float32)
+    at = np.float32(0.3)
+    assert float(at) > 0.3                                   # float64: above the bound
+    assert val(np.array([at, 0.0], np.float32), pos, pos)[0]   # float32 (NEP 50): on it -> valid
+    up = np.nextafter(at, np.float32(1.0))
+    assert not val(np.array([up, 0.0], np.float32), pos, pos)[0]
+    lo = np.float32(0.1)                                     # f32(0.1) > 0.1: the lower bound the same way
+    assert val(np.array([lo, 0.0], np.float32), pos, pos)[0]
+    assert not val(np.array([np.nextafter(lo, np.float32(0.0)), 0.0], np.float32), pos, pos)[0]
