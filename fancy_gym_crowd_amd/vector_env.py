@@ -446,6 +446,10 @@ class StepVectorEnv:
     def get_state(self):
         return BlackBoxVectorEnv.get_state(self)
 
+    def set_state(self, q=None, qd=None, goal=None, hole=None, steps=None):
+        """fgx_set_state (checkpoint restore / tests), as BlackBoxVectorEnv.set_state."""
+        return BlackBoxVectorEnv.set_state(self, q, qd, goal, hole, steps)
+
     def close(self):
         self._eng.close()
 

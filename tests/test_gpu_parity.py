@@ -43,7 +43,8 @@ def spec_of(env):
     return mp.MPSpec(kind=kind, dof=c.n_links, n_basis=c.n_basis, phase="linear" if c.phase_kind == 0 else "exp",
                      tau=c.tau, delay=c.delay, alpha_phase=c.alpha_phase, bandwidth=c.bandwidth,
                      zero_start=c.zero_start, zero_goal=c.zero_goal, basis_outside=c.num_basis_outside, weights_scale=c.weights_scale,
-                     goal_scale=c.goal_scale, alpha=c.alpha, pc_length=c.pc_length, dt=c.dt, duration=c.duration)
+                     goal_scale=c.goal_scale, alpha=c.alpha, pc_length=c.pc_length, dt=c.dt, duration=c.duration,
+                     basis_dt=c.basis_dt if c.mp_kind == 3 else 0.0)
 
 
 def ctrl_of(env):
@@ -621,3 +622,40 @@ def test_trajectory_mfma_equals_valu(env_id, N, monkeypatch):
         for a, b in zip(outs[0], other):
             assert a.shape == b.shape
             np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("env_id,over", [
+    ("fancy_ProDMP/HoleReacher-v0", {"basis_generator_kwargs": {"dt": 0.005}}),
+    ("fancy_ProDMP/SimpleReacher-v0", {"basis_generator_kwargs": {"dt": 0.02}}),
+    ("fancy_ProDMP/LongSimpleReacher-v0", {"basis_generator_kwargs": {"dt": 0.0075},
+                                           "phase_generator_kwargs": {"delay": 0.2}}),
+    ("fancy_ProMP/LongSimpleReacher-v0", {"phase_generator_kwargs": {"delay": -0.25}}),   # negative delay: ProMP
+    ("fancy_DMP/SimpleReacher-v0", {"phase_generator_kwargs": {"delay": -0.1}}),          # and DMP accept it
+])
+def test_basis_dt_and_negative_delay_vs_oracle(env_id, over):
+    """A ProDMP basis generator dt of its own (basis_generator_factory.py:8-23; its precompute grid,
+    looked up at the rounded grid index of each env step) and a negative phase delay for ProMP / DMP
+    (the phase clips max((t - delay) / tau, 0); fgx_create refuses a negative delay only for ProDMP):
+    tables bit-exact, then BB steps end to end against the oracle."""
+    N = 256
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    spec = spec_of(env)
+    got = np_(env.tables())
+    ref = oracle_tables(spec, got.shape[0])
+    np.testing.assert_array_equal(got[:, :ref.shape[1]].view(np.uint32), ref.view(np.uint32))
+    ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, **oracle_kwargs(env))
+    close(np_(env.reset(seed=4)[0]), ob.reset(seed=4))
+    rng = np.random.default_rng(9)
+    for _ in range(2):
+        params = rng.standard_normal((N, env.n_params), dtype=np.float32)
+        obs, ret, te, tr, info = env.step(torch.from_numpy(params).to(DEV))
+        r_obs, r_ret, r_te, r_tr, r_info = ob.step(params)
+        np.testing.assert_array_equal(np_(info["trajectory_length"]), r_info["trajectory_length"])
+        np.testing.assert_array_equal(np_(te).astype(bool), r_te)
+        np.testing.assert_array_equal(np_(tr).astype(bool), r_tr)
+        assert_ulps(np_(ret), r_ret, 16)
+        close(np_(obs), r_obs)
+        np.testing.assert_array_equal(np_(env.get_state()["q"]), ob.env.q)
+    with pytest.raises(ValueError):   # ProDMP keeps refusing a negative delay
+        fgx.make("fancy_ProDMP/SimpleReacher-v0", num_envs=8, device=DEV,
+                 mp_config_override={"phase_generator_kwargs": {"delay": -0.1}})
