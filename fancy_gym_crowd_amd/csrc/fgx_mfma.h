@@ -196,23 +196,27 @@ __global__ __launch_bounds__(64 * kTrajWaves) void k_traj_mfma_r3(DevCfg c, DevS
 // kernel writing every env's 4000-B [T, dof] run as 160..2000-B pieces (a tile loop's order) reaches
 // 3.2-4.3 TB/s on the box, the same runs written whole 5.2 TB/s, the 128-KB region of 32 envs
 // linearly 5.4-5.6 TB/s (tools/wbench.hip, profiles/r04_wbench.jsonl).  So here a workgroup owns GE
-// envs and writes their runs whole:
-//   * its 8 waves compute one 32-row tile each (a segment of 8 tiles covers T = 200) into an LDS
-//     region [env][row][dof] (GE x T x dof floats; 64 KB at GE = 16, two workgroups per CU), one
-//     workgroup barrier (an LDS-only one: s_barrier after lgkmcnt(0), not __syncthreads, whose
-//     fence would wait for the outstanding global stores), then every wave streams whole env runs
-//     out with 16-B stores (consecutive lanes on consecutive chunks) — positions, then velocities;
+// envs and writes their runs whole (ProMP 184 -> 112.5 us = 4.7 TB/s, ProDMP 145 -> 139.6 us at
+// 65536 envs, profiles/r04_traj_ab_s2.txt):
+//   * one 8-wave workgroup per CU walks 32-env groups; per group its waves compute one 32-row tile
+//     each (a segment of 8 tiles covers T = 200) into an LDS region [env][row][dof] (32 x T x dof
+//     floats, 128 KB), one workgroup barrier (an LDS-only one: s_barrier after lgkmcnt(0), not
+//     __syncthreads, whose fence would wait for the outstanding global stores), then waves 0..6
+//     stream whole env runs out with 16-B stores (consecutive lanes on consecutive chunks) —
+//     positions, then velocities;
+//   * wave 7 stores nothing: it loads the next group's weights (and ProDMP's q0 / qd0) into LDS, so
+//     no load waits behind the stores (vmcnt counts loads and stores in one queue); the basis table
+//     sits in LDS for the same reason;
 //   * ProMP computes each position once: the forward difference takes row k + 1 from the next
 //     register of the lane, or for the last row of a lane's 4-row group from the other half-wave
 //     (v_permlane32_swap: rows 8g + 4 .. 8g + 7 live in lanes 32..63); a tile outputs its first 28
 //     rows (the 28th's successor is in the tile), the plan's last tile all its remaining rows
 //     (velocity of the last = the previous one, as Traj::at).  ProDMP's velocities are their own
-//     contraction (the second basis, vb), computed into the same accumulators after the positions
-//     left; its tiles step 32 rows;
-//   * the basis table sits in LDS: no global load follows a global store (vmcnt counts both, so a
-//     load behind the stores would wait for them).
-// With GE = 16 the MFMA's env columns 16..31 are computed and dropped (the matrix pipe has ample
-// slack: 2 flop per output byte).
+//     contraction (the second basis, vb), computed into the position accumulators once the
+//     positions left; its tiles step 32 rows.
+// (Tried and slower: 16-env groups at two workgroups per CU, 123 us; 4 compute + 4 store waves
+// with double-buffered 16-env halves, 171 us; velocities held in registers across the position
+// stores, ProDMP 141.6 us.)
 constexpr int kTrajGWaves = 8;   // waves (tiles of a segment) per workgroup
 constexpr int kTrajGE = 32;      // envs per group (the MFMA's columns)
 
@@ -361,12 +365,12 @@ __global__ __launch_bounds__(64 * kTrajGWaves) void k_traj_mfma(DevCfg c, DevSta
       const int rows_out = (t == nt - 1) ? T - tb : RSTEP;   // multiple of 4
       // lane (j, h) holds rows 8g + 4h + {0..3} of the tile (registers 4g + {0..3}); its LDS rows
       float* dst0 = reg + j * ESR + (tb - row0 + 4 * h) * NL;
-      f32x16 cp[NL], cv[NL];   // positions, velocities
+      f32x16 cp[NL], cv[PRO ? NL : 1];   // positions, ProMP velocities
+      float a1[4], a2[4];
       if (has_tile) {
         // ---- A operands: this lane feeds time row i = j of the tile, k = 2 sidx + h
         const int ktc = min(tb + j, T - 1);
         const float* ar = tab + (size_t)(ktc + 1) * stride;   // table row (s0 = 0)
-        float a1[4], a2[4];
 #pragma unroll
         for (int sidx = 0; sidx < 4; ++sidx) {
           const int kk = 2 * sidx + h;
@@ -384,13 +388,6 @@ __global__ __launch_bounds__(64 * kTrajGWaves) void k_traj_mfma(DevCfg c, DevSta
           cp[d] = z;
 #pragma unroll
           for (int sidx = 0; sidx < 4; ++sidx) cp[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[sidx], bco[d][sidx], cp[d], 0, 0, 0);
-          if constexpr (!PRO) {
-            cv[d] = z;
-#pragma unroll
-            for (int sidx = 0; sidx < 4; ++sidx) cv[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sidx], bco[d][sidx], cv[d], 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cv[d][r] = div_rcp(cv[d][r], c.tau32, c.rcp_tau32);
-          }
         }
         if constexpr (PRO) {
 #pragma unroll
@@ -443,7 +440,22 @@ __global__ __launch_bounds__(64 * kTrajGWaves) void k_traj_mfma(DevCfg c, DevSta
       lds_barrier();
       store_region(dpos, row0, rows);
       lds_barrier();   // (every wave's region reads done before the velocities overwrite it)
-      stage(cv);
+      if constexpr (PRO) {
+        stage(cv);
+      } else {   // ProDMP velocities: the second contraction, into the position accumulators
+        if (has_tile) {
+#pragma unroll
+          for (int d = 0; d < NL; ++d) {
+            f32x16 z = {0.0f};
+            cp[d] = z;
+#pragma unroll
+            for (int sidx = 0; sidx < 4; ++sidx) cp[d] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sidx], bco[d][sidx], cp[d], 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cp[d][r] = div_rcp(cp[d][r], c.tau32, c.rcp_tau32);
+          }
+        }
+        stage(cp);
+      }
       lds_barrier();
       store_region(dvel, row0, rows);
       lds_barrier();
