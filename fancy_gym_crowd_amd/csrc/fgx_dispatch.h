@@ -210,7 +210,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
         return -2;
       }
       hipLaunchKernelGGL((k_episode_v2<MP, NL, NB>), dim3((unsigned)((c.N + 64 * kV2Pairs - 1) / (64 * kV2Pairs))),
-                         dim3(128 * kV2Pairs), lv, stream, c, s, params, o);
+                         dim3(kV2Threads), lv, stream, c, s, params, o);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) { err = std::string("k_episode_v2 launch: ") + hipGetErrorString(e); return -2; }
       return 0;

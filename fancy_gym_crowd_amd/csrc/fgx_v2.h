@@ -42,7 +42,13 @@ __device__ __forceinline__ void st_row(T* A, int64_t r, int64_t N, uint32_t eb, 
   gchar* rb = uniform_ptr(A + r * N);
   *(__attribute__((address_space(1))) T*)(rb + eb) = x;
 }
-constexpr int kV2Pairs = 4;   // dynamics / observation wave pairs per workgroup (256 envs)
+constexpr int kV2Pairs = 4;   // dynamics / observation wave sets per workgroup (256 envs)
+#ifdef FGX_V2_TWO_OBS   // A/B builds only: two observation waves per dynamics wave (FK / end effector, and
+constexpr int kV2Obs = 2;   // cos / sin of q): three waves per SIMD cap registers at 168, and the dynamics
+#else                       // wave then spills (154 VGPRs at 5 links)
+constexpr int kV2Obs = 1;   // observation waves per dynamics wave
+#endif
+constexpr int kV2Threads = 64 * kV2Pairs * (1 + kV2Obs);
 
 inline size_t v2_lds_bytes(int rows, int stride, int nl) {
   return (((size_t)rows * stride + 3) & ~(size_t)3) * sizeof(float) +
@@ -50,7 +56,7 @@ inline size_t v2_lds_bytes(int rows, int stride, int nl) {
 }
 
 template <int MP, int NL, int NB>
-__global__ __launch_bounds__(512) void k_episode_v2(DevCfg c, DevState s, const float* __restrict__ params,
+__global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s, const float* __restrict__ params,
                                                     Outputs o) {
   constexpr int C = kV2Chunk;
   extern __shared__ float4 lds_v2[];
@@ -62,7 +68,8 @@ __global__ __launch_bounds__(512) void k_episode_v2(DevCfg c, DevState s, const 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool obs_wave = w >= kV2Pairs;
-  const int pair = w & (kV2Pairs - 1);
+  const int pair = w & (kV2Pairs - 1);   // (waves w, w + 4, w + 8 share a SIMD)
+  const int obs_role = kV2Obs == 1 ? 0 : (w >= 2 * kV2Pairs ? 2 : 1);   // 0: all, 1: FK, 2: cos / sin of q
   const int64_t N = c.N;
   const int64_t e0 = (int64_t)blockIdx.x * (64 * kV2Pairs) + pair * 64 + lane;
   const bool valid = e0 < N;
@@ -90,32 +97,112 @@ __global__ __launch_bounds__(512) void k_episode_v2(DevCfg c, DevState s, const 
     // write chunk it into the other buffer
     for (int it = 0; it <= nch; ++it) {
       const int ch = it - 1, b = ch & 1;
+#ifdef FGX_V2_ABL_OBS   // A/B builds only: the observation waves idle
+      if (false) {
+#else
       if (it > 0 && so && valid) {
+#endif
 #pragma unroll
         for (int i = 0; i < C; ++i) {
           const int k = ch * C + i;
           if (k >= T) break;
-          if (k < sg.L) {   // cos / sin of q (q[0]'s from FK), end effector - goal: k_info_obs's code
+          const bool fk_part = obs_role != 2, q_part = obs_role != 1;
+          if (k < sg.L && kV2Obs == 1) {
+            // cos / sin of q (q[0]'s from FK) and end effector - goal, the f32 values k_info_obs
+            // computes: a fast path (fgx_sincos_fast; the cumulative angles' cos / sin by angle
+            // addition) whose every f32 result is checked against its error bound, else the lane
+            // recomputes them exactly
+            double q[NL], cq[NL], sq[NL];
+            bool ok = true;
+#pragma unroll
+            for (int d = 0; d < NL; ++d) {
+              q[d] = rq(b, i, d);
+              ok = ok && __builtin_fabs(q[d]) < 0x1p20;   // (and not NaN)
+              fgx_sincos_fast(q[d], &sq[d], &cq[d]);
+            }
+            float out[2 * NL + 2];
+            // |fast - exact| <= 5e-16 + 1.1e-16 (the exact path's own error) for cos / sin of q
+            constexpr double kTrigM = 1e-15;
+            // end effector: link d's cos / sin carry the d angle additions' product roundings
+            // (~3e-16 each) and the exact path's roundings of the cumulative angles (<= 1.1e-16 A
+            // each, A = sum |q| >= every |angle|); summed over the links and with the sums' own
+            // roundings, < NL^2 / 2 (1.1e-16 A + 3e-16) + 4.4e-16 NL: the margin doubles that
+            double A = 0.0;
+#pragma unroll
+            for (int d = 0; d < NL; ++d) A += __builtin_fabs(q[d]);
+            const double kEeM = NL * NL * (2e-16 * A + 1e-15) + 1e-14;
+            double C = cq[0], S = sq[0], x = cq[0], y = sq[0];
+#pragma unroll
+            for (int d = 1; d < NL; ++d) {
+              const double C2 = __builtin_fma(C, cq[d], -(S * sq[d]));
+              const double S2 = __builtin_fma(S, cq[d], C * sq[d]);
+              C = C2;
+              S = S2;
+              x = x + C;
+              y = y + S;
+            }
+#pragma unroll
+            for (int d = 0; d < NL; ++d) {
+              out[d] = f32_checked(cq[d], kTrigM, ok);
+              out[NL + d] = f32_checked(sq[d], kTrigM, ok);
+            }
+            out[2 * NL] = f32_checked((0.0 + x) - gx, kEeM, ok);
+            out[2 * NL + 1] = f32_checked((0.0 + y) - gy, kEeM, ok);
+            if (!ok) {   // (rare: a value near an f32 rounding boundary, or |q| >= 2^20)
+              Env<NL> v;
+#pragma unroll
+              for (int d = 0; d < NL; ++d) v.q[d] = q[d];
+              v.fk();
+              out[0] = (float)v.c[0];
+              out[NL] = (float)v.s[0];
+#pragma unroll
+              for (int d = 1; d < NL; ++d) {
+                double sn, cs;
+                fgx_sincos(v.q[d], &sn, &cs);
+                out[d] = (float)cs;
+                out[NL + d] = (float)sn;
+              }
+              out[2 * NL] = (float)(v.jx[NL] - gx);
+              out[2 * NL + 1] = (float)(v.jy[NL] - gy);
+            }
+#pragma unroll
+            for (int p = 0; p < 2 * NL; ++p) st_row(so, row_of(k, p), N, e4, out[p]);
+            st_row(so, row_of(k, 3 * NL), N, e4, out[2 * NL]);
+            st_row(so, row_of(k, 3 * NL + 1), N, e4, out[2 * NL + 1]);
+          } else if (k < sg.L) {   // (two observation waves: the exact path, split)
             Env<NL> v;
 #pragma unroll
             for (int d = 0; d < NL; ++d) v.q[d] = rq(b, i, d);
-            v.fk();
-            st_row(so, row_of(k, 0), N, e4, (float)v.c[0]);
-            st_row(so, row_of(k, NL), N, e4, (float)v.s[0]);
-#pragma unroll
-            for (int d = 1; d < NL; ++d) {
-              double sn, cs;
-              fgx_sincos(v.q[d], &sn, &cs);
-              st_row(so, row_of(k, d), N, e4, (float)cs);
-              st_row(so, row_of(k, NL + d), N, e4, (float)sn);
+            if (fk_part) {
+              v.fk();
+              st_row(so, row_of(k, 0), N, e4, (float)v.c[0]);
+              st_row(so, row_of(k, NL), N, e4, (float)v.s[0]);
+              st_row(so, row_of(k, 3 * NL), N, e4, (float)(v.jx[NL] - gx));
+              st_row(so, row_of(k, 3 * NL + 1), N, e4, (float)(v.jy[NL] - gy));
             }
-            st_row(so, row_of(k, 3 * NL), N, e4, (float)(v.jx[NL] - gx));
-            st_row(so, row_of(k, 3 * NL + 1), N, e4, (float)(v.jy[NL] - gy));
-          } else {
+            if (q_part) {
 #pragma unroll
-            for (int p = 0; p < 2 * NL; ++p) st_row(so, row_of(k, p), N, e4, fnan);
-            st_row(so, row_of(k, 3 * NL), N, e4, fnan);
-            st_row(so, row_of(k, 3 * NL + 1), N, e4, fnan);
+              for (int d = 1; d < NL; ++d) {
+                double sn, cs;
+                fgx_sincos(v.q[d], &sn, &cs);
+                st_row(so, row_of(k, d), N, e4, (float)cs);
+                st_row(so, row_of(k, NL + d), N, e4, (float)sn);
+              }
+            }
+          } else {
+            if (fk_part) {
+              st_row(so, row_of(k, 0), N, e4, fnan);
+              st_row(so, row_of(k, NL), N, e4, fnan);
+              st_row(so, row_of(k, 3 * NL), N, e4, fnan);
+              st_row(so, row_of(k, 3 * NL + 1), N, e4, fnan);
+            }
+            if (q_part) {
+#pragma unroll
+              for (int d = 1; d < NL; ++d) {
+                st_row(so, row_of(k, d), N, e4, fnan);
+                st_row(so, row_of(k, NL + d), N, e4, fnan);
+              }
+            }
           }
         }
       }
@@ -154,6 +241,25 @@ __global__ __launch_bounds__(512) void k_episode_v2(DevCfg c, DevState s, const 
   auto row = [&](int k, int b, int i) __attribute__((always_inline)) {
     float pos[NL], vel[NL];
     tg.at(c, k, pos, vel);
+#ifdef FGX_V2_ABL_DYNST   // A/B builds only: the dynamics waves store no per-sample rows
+    if (valid && k < L) {
+      double a[NL];
+      float a32[NL];
+#pragma unroll
+      for (int d = 0; d < NL; ++d) {
+        const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
+        const double cl = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
+        a[d] = (u != u) ? u : cl;
+        a32[d] = 0.0f;
+      }
+      const StepOut r = substep<ENV_SIMPLE, false, NL, true>(c, v, a, a32, false);
+      trunc = v.steps >= c.max_steps;
+      ps.add(k, r.reward, split);
+#pragma unroll
+      for (int d = 0; d < NL; ++d) rq(b, i, d) = v.q[d];
+    }
+    return;
+#endif
     if (!valid) return;
     if (oo.positions) {
 #pragma unroll
