@@ -141,3 +141,36 @@ def test_v2_equals_logging_kernel(ci, info_level, N, monkeypatch):
         sa, sb = a.get_state(), b.get_state()
         for k in sa:
             np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)
+
+
+@pytest.mark.parametrize("env_id", ["fancy_ProMP/LongSimpleReacher-v0", "fancy_ProMP/SimpleReacher-v0"])
+def test_v2_observation_fallback_lanes(env_id, monkeypatch):
+    """k_episode_v2's observation fast path (fgx_sincos_fast + angle-addition FK, each f32 result
+    checked against its error bound) and its exact recompute, lane by lane: joint angles beyond the
+    fast reduction's range (|q| >= 2^20), angles whose sin / cos round below f32 resolution of the
+    margin (q ~ 1e-9, q0 = pi / 2) and ordinary lanes in the same waves; every observation row bit for
+    bit against the logging k_episode + k_info_obs (exact sincos throughout)."""
+    N = 640
+    a = fgx.make(env_id, num_envs=N, device=DEV)
+    b = fgx.make(env_id, num_envs=N, device=DEV)
+    assert a.episode_kernel() == "k_episode_v2"
+    a.reset(seed=3)
+    b.reset(seed=3)
+    rng = np.random.default_rng(7)
+    st = a.get_state()
+    q = np_(st["q"]).copy()
+    q[0:N:5] = rng.choice([-1.0, 1.0], q[0:N:5].shape) * 10.0 ** rng.uniform(6.5, 9, q[0:N:5].shape)
+    q[1:N:5] = rng.uniform(-1e-9, 1e-9, q[1:N:5].shape)
+    q[2:N:5, 0] = np.pi / 2
+    qd = np.zeros_like(q)
+    for e in (a, b):
+        e.set_state(q=q, qd=qd)
+    p = torch.from_numpy((rng.standard_normal((N, a.n_params)) * 0.01).astype(np.float32)).to(DEV)
+    monkeypatch.delenv("FGX_V2", raising=False)
+    ra = a.step(p)
+    monkeypatch.setenv("FGX_V2", "0")
+    rb = b.step(p)
+    monkeypatch.delenv("FGX_V2")
+    np.testing.assert_array_equal(np_(ra[0]), np_(rb[0]))
+    np.testing.assert_array_equal(np_(ra[4]["step_observations"]), np_(rb[4]["step_observations"]))
+    assert np.isfinite(np_(ra[4]["step_observations"])[:, :10]).all()
