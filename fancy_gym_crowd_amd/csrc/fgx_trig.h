@@ -83,7 +83,7 @@ __device__ __forceinline__ void fgx_sincos(double x, double* sp, double* cp) {
 // through r^15 / r^16 on |r| <= pi/4 (truncation < 5e-17), ~30 VALU instead of ~50.  For results
 // that are then rounded to f32 and checked against that error (f32_checked below): equal to the
 // exact path's f32 whenever the check passes.
-__device__ __forceinline__ void fgx_sincos_fast(double x, double* sp, double* cp) {
+__host__ __device__ __forceinline__ void fgx_sincos_fast(double x, double* sp, double* cp) {
   const double k = __builtin_rint(x * 0x1.45f306dc9c883p-1);                 // x * 2 / pi
   double r = __builtin_fma(-k, 0x1.921fb54442d18p+0, x);                     // pi / 2 (hi)
   r = __builtin_fma(-k, 0x1.1a62633145c07p-54, r);                           // pi / 2 (lo)
@@ -112,10 +112,53 @@ __device__ __forceinline__ void fgx_sincos_fast(double x, double* sp, double* cp
 
 // (float) v where v is within m of the exact value whose (float) is wanted: both ends of [v - m, v + m]
 // round alike, or ok is cleared (the caller recomputes exactly)
-__device__ __forceinline__ float f32_checked(double v, double m, bool& ok) {
+__host__ __device__ __forceinline__ float f32_checked(double v, double m, bool& ok) {
   const float lo = (float)(v - m), hi = (float)(v + m);
   ok = ok && (lo == hi);
   return lo;
+}
+
+// The observation's trigonometric components of one sample (emit_obs / k_info_obs order: cos q[0..NL),
+// sin q[0..NL), end effector x - gx, y - gy) as f32, from the fast path: fgx_sincos_fast of every
+// joint angle, the cumulative angles' cos / sin by angle addition, the end effector as the same
+// sequential sums, every f32 through f32_checked.  Returns false if any value could round otherwise
+// than the exact path's (Env::fk + fgx_sincos) — or |q| >= 2^20, or NaN: the caller recomputes then.
+//   cos / sin of q: |fast - exact| <= 1.5e-16 + the exact path's own <= 1 ulp: margin 1e-15;
+//   end effector: link d's cos / sin carry d angle additions' product roundings (~3e-16 each) and
+//   the exact path's roundings of the cumulative angles (<= 1.1e-16 A each, A = sum |q| >= every
+//   |angle|); summed over the links with the sums' own roundings, < NL^2 / 2 (1.1e-16 A + 3e-16) +
+//   4.4e-16 NL: the margin doubles that.
+template <int NL>
+__host__ __device__ __forceinline__ bool obs_trig_fast(const double* q, double gx, double gy, float* out) {
+  double cq[NL], sq[NL];
+  bool ok = true;
+  double A = 0.0;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) {
+    ok = ok && __builtin_fabs(q[d]) < 0x1p20;   // (and not NaN)
+    fgx_sincos_fast(q[d], &sq[d], &cq[d]);
+    A += __builtin_fabs(q[d]);
+  }
+  constexpr double kTrigM = 1e-15;
+  const double kEeM = NL * NL * (2e-16 * A + 1e-15) + 1e-14;
+  double ca = cq[0], sa = sq[0], x = cq[0], y = sq[0];   // cos / sin of the cumulative angle
+#pragma unroll
+  for (int d = 1; d < NL; ++d) {
+    const double c2 = __builtin_fma(ca, cq[d], -(sa * sq[d]));
+    const double s2 = __builtin_fma(sa, cq[d], ca * sq[d]);
+    ca = c2;
+    sa = s2;
+    x = x + ca;
+    y = y + sa;
+  }
+#pragma unroll
+  for (int d = 0; d < NL; ++d) {
+    out[d] = f32_checked(cq[d], kTrigM, ok);
+    out[NL + d] = f32_checked(sq[d], kTrigM, ok);
+  }
+  out[2 * NL] = f32_checked((0.0 + x) - gx, kEeM, ok);
+  out[2 * NL + 1] = f32_checked((0.0 + y) - gy, kEeM, ok);
+  return ok;
 }
 
 }  // namespace fgx

@@ -10,20 +10,23 @@
 // per sample and env, ~0.27 ms of full-chip VALU issue).  The logging k_episode puts
 // both in one lone wave per SIMD; here they run side by side on the same SIMD:
 //   waves 0..3 ("dynamics", one env per lane as k_episode): trajectory, PD, clip, torque Euler step,
-//     reward, the numpy pairwise return, the epilogue (final observation, TimeLimit, auto-reset), and
-//     per sample the rows that need no trigonometry: positions, velocities, step_actions,
-//     step_rewards, reward_dist, reward_ctrl and the observation's q̇ / step / time components, each
-//     a store of 64 consecutive envs ([T, X, N] rows, include/fgx.h fgx_info); q goes to an LDS ring;
-//   waves 4..7 ("observation", the same 64 envs): per sample FK of the staged q and cos / sin of
-//     every q — the same Env::fk / fgx_sincos / conversions as emit_obs and k_info_obs — and the
-//     observation's trigonometric and end-effector components.
+//     reward, the epilogue (final observation, TimeLimit, auto-reset), and per sample the rows that
+//     need no trigonometry: positions, velocities, step_actions, step_rewards, reward_dist,
+//     reward_ctrl and the observation's q̇ / step / time components, each a store of 64 consecutive
+//     envs ([T, X, N] rows, include/fgx.h fgx_info); q and the reward go to an LDS ring;
+//   waves 4..7 ("observation", the same 64 envs): per sample the observation's trigonometric and
+//     end-effector components from the staged q (an exact-checked fast path, DESIGN.md §4.9, else
+//     the same Env::fk / fgx_sincos as emit_obs and k_info_obs), and the numpy pairwise return of the
+//     staged rewards (handed back through LDS for the epilogue: its accumulators stay off the
+//     dynamics waves' registers, which would otherwise spill — and a spill reload waits behind the
+//     wave's outstanding stores, vmcnt counting both).
 // Wave w and wave w + 4 of a workgroup share a SIMD (profiles/r01_wave_placement.txt), so each SIMD
 // interleaves one dynamics and one observation wave; the ring holds kV2Chunk samples, double-buffered,
 // one workgroup barrier per chunk (the k_episode_ws protocol with the roles' work reversed).
 //
-// Every value is computed by the same expressions as the logging k_episode (+ k_info_obs):
-// bit-identical results (tests/test_gpu_info_rows.py).  Served: ENV_SIMPLE + PD + shared tables,
-// static replanning schedules, max_episode_steps <= 200, no validity checks (fgx_dispatch.h).
+// Every value equals the logging k_episode's (+ k_info_obs): bit-identical results
+// (tests/test_gpu_info_rows.py).  Served: ENV_SIMPLE + PD + shared tables, static replanning
+// schedules, max_episode_steps <= 200, no validity checks (fgx_dispatch.h).
 #pragma once
 #include "fgx_jp.h"
 
@@ -42,17 +45,14 @@ __device__ __forceinline__ void st_row(T* A, int64_t r, int64_t N, uint32_t eb, 
   gchar* rb = uniform_ptr(A + r * N);
   *(__attribute__((address_space(1))) T*)(rb + eb) = x;
 }
-constexpr int kV2Pairs = 4;   // dynamics / observation wave sets per workgroup (256 envs)
-#ifdef FGX_V2_TWO_OBS   // A/B builds only: two observation waves per dynamics wave (FK / end effector, and
-constexpr int kV2Obs = 2;   // cos / sin of q): three waves per SIMD cap registers at 168, and the dynamics
-#else                       // wave then spills (154 VGPRs at 5 links)
-constexpr int kV2Obs = 1;   // observation waves per dynamics wave
-#endif
-constexpr int kV2Threads = 64 * kV2Pairs * (1 + kV2Obs);
+constexpr int kV2Pairs = 4;   // dynamics / observation wave pairs per workgroup (256 envs)
+constexpr int kV2Threads = 128 * kV2Pairs;
 
+// LDS: the basis table, the ring ([pair][2][C][NL + 1][64] doubles: q and the reward of each sample)
+// and each env's return
 inline size_t v2_lds_bytes(int rows, int stride, int nl) {
   return (((size_t)rows * stride + 3) & ~(size_t)3) * sizeof(float) +
-         (size_t)kV2Pairs * 2 * kV2Chunk * nl * 64 * sizeof(double);
+         (size_t)kV2Pairs * 2 * kV2Chunk * (nl + 1) * 64 * sizeof(double) + (size_t)kV2Pairs * 64 * sizeof(double);
 }
 
 template <int MP, int NL, int NB>
@@ -62,20 +62,21 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
   extern __shared__ float4 lds_v2[];
   float* tab = (float*)lds_v2;
   const int tab_f = c.rows * c.stride;
-  double* ring = (double*)(lds_v2 + (tab_f + 3) / 4);   // [pair][2][C][NL][64]
+  constexpr int RS = NL + 1;   // ring doubles per sample and lane: q, then the reward
+  double* ring = (double*)(lds_v2 + (tab_f + 3) / 4);   // [pair][2][C][RS][64]
+  double* rets = ring + (size_t)kV2Pairs * 2 * C * RS * 64;   // [pair][64]
   for (int i = threadIdx.x; i < tab_f; i += blockDim.x) tab[i] = s.tables[i];
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool obs_wave = w >= kV2Pairs;
-  const int pair = w & (kV2Pairs - 1);   // (waves w, w + 4, w + 8 share a SIMD)
-  const int obs_role = kV2Obs == 1 ? 0 : (w >= 2 * kV2Pairs ? 2 : 1);   // 0: all, 1: FK, 2: cos / sin of q
+  const int pair = w & (kV2Pairs - 1);   // (waves w and w + 4 share a SIMD)
   const int64_t N = c.N;
   const int64_t e0 = (int64_t)blockIdx.x * (64 * kV2Pairs) + pair * 64 + lane;
   const bool valid = e0 < N;
   const int64_t e = valid ? e0 : N - 1;   // clamped index: loads stay in bounds, nothing is stored
-  double* myring = ring + (size_t)pair * 2 * C * NL * 64;
-  auto rq = [&](int b, int i, int d) __attribute__((always_inline)) -> double& { return myring[((b * C + i) * NL + d) * 64 + lane]; };
+  double* myring = ring + (size_t)pair * 2 * C * RS * 64;
+  auto rq = [&](int b, int i, int d) __attribute__((always_inline)) -> double& { return myring[((b * C + i) * RS + d) * 64 + lane]; };
   const int T = c.T;
   const int nch = (T + C - 1) / C;   // every wave walks all T rows (the plan rows continue after L)
   const int X = c.full_dim;
@@ -87,67 +88,40 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
 
   JpSeg sg;
   sg.init(c, s, e, valid);
+  const int L = sg.L;
+  // numpy pairwise split of the return sum (SimpleReacher never terminates: L is known now)
+  const int split = (L > 128) ? ((L / 2) & ~7) : 0;
   __syncthreads();   // table staged
 
   if (obs_wave) {
     // ------------------------------------------------------------------ observation waves
     const double gx = s.goal[e], gy = s.goal[N + e];   // the episode's goal (the auto-reset comes later)
     float* so = o.step_obs;
+    // the episode return: numpy's pairwise sum of the rewards the dynamics waves stage (its 19
+    // accumulators live here, off the dynamics waves' registers)
+    PairwiseSum ps;
+    ps.init();
     // iteration it reads chunk it - 1 (staged before the previous barrier) while the dynamics waves
     // write chunk it into the other buffer
     for (int it = 0; it <= nch; ++it) {
       const int ch = it - 1, b = ch & 1;
-#ifdef FGX_V2_ABL_OBS   // A/B builds only: the observation waves idle
-      if (false) {
-#else
-      if (it > 0 && so && valid) {
-#endif
+      if (it > 0 && valid) {
 #pragma unroll
         for (int i = 0; i < C; ++i) {
           const int k = ch * C + i;
           if (k >= T) break;
-          const bool fk_part = obs_role != 2, q_part = obs_role != 1;
-          if (k < sg.L && kV2Obs == 1) {
+          if (k < L) ps.add(k, rq(b, i, NL), split);
+          if (!so) continue;
+          if (k < L) {
             // cos / sin of q (q[0]'s from FK) and end effector - goal, the f32 values k_info_obs
             // computes: a fast path (fgx_sincos_fast; the cumulative angles' cos / sin by angle
             // addition) whose every f32 result is checked against its error bound, else the lane
-            // recomputes them exactly (DESIGN.md §4.10)
-            double q[NL], cq[NL], sq[NL];
-            bool ok = true;
+            // recomputes them exactly (DESIGN.md §4.9)
+            double q[NL];
 #pragma unroll
-            for (int d = 0; d < NL; ++d) {
-              q[d] = rq(b, i, d);
-              ok = ok && __builtin_fabs(q[d]) < 0x1p20;   // (and not NaN)
-              fgx_sincos_fast(q[d], &sq[d], &cq[d]);
-            }
+            for (int d = 0; d < NL; ++d) q[d] = rq(b, i, d);
             float out[2 * NL + 2];
-            // |fast - exact| <= 5e-16 + 1.1e-16 (the exact path's own error) for cos / sin of q
-            constexpr double kTrigM = 1e-15;
-            // end effector: link d's cos / sin carry the d angle additions' product roundings
-            // (~3e-16 each) and the exact path's roundings of the cumulative angles (<= 1.1e-16 A
-            // each, A = sum |q| >= every |angle|); summed over the links and with the sums' own
-            // roundings, < NL^2 / 2 (1.1e-16 A + 3e-16) + 4.4e-16 NL: the margin doubles that
-            double A = 0.0;
-#pragma unroll
-            for (int d = 0; d < NL; ++d) A += __builtin_fabs(q[d]);
-            const double kEeM = NL * NL * (2e-16 * A + 1e-15) + 1e-14;
-            double C = cq[0], S = sq[0], x = cq[0], y = sq[0];
-#pragma unroll
-            for (int d = 1; d < NL; ++d) {
-              const double C2 = __builtin_fma(C, cq[d], -(S * sq[d]));
-              const double S2 = __builtin_fma(S, cq[d], C * sq[d]);
-              C = C2;
-              S = S2;
-              x = x + C;
-              y = y + S;
-            }
-#pragma unroll
-            for (int d = 0; d < NL; ++d) {
-              out[d] = f32_checked(cq[d], kTrigM, ok);
-              out[NL + d] = f32_checked(sq[d], kTrigM, ok);
-            }
-            out[2 * NL] = f32_checked((0.0 + x) - gx, kEeM, ok);
-            out[2 * NL + 1] = f32_checked((0.0 + y) - gy, kEeM, ok);
+            const bool ok = obs_trig_fast<NL>(q, gx, gy, out);
             if (!ok) {   // (rare: a value near an f32 rounding boundary, or |q| >= 2^20)
               Env<NL> v;
 #pragma unroll
@@ -169,45 +143,18 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
             for (int p = 0; p < 2 * NL; ++p) st_row(so, row_of(k, p), N, e4, out[p]);
             st_row(so, row_of(k, 3 * NL), N, e4, out[2 * NL]);
             st_row(so, row_of(k, 3 * NL + 1), N, e4, out[2 * NL + 1]);
-          } else if (k < sg.L) {   // (two observation waves: the exact path, split)
-            Env<NL> v;
-#pragma unroll
-            for (int d = 0; d < NL; ++d) v.q[d] = rq(b, i, d);
-            if (fk_part) {
-              v.fk();
-              st_row(so, row_of(k, 0), N, e4, (float)v.c[0]);
-              st_row(so, row_of(k, NL), N, e4, (float)v.s[0]);
-              st_row(so, row_of(k, 3 * NL), N, e4, (float)(v.jx[NL] - gx));
-              st_row(so, row_of(k, 3 * NL + 1), N, e4, (float)(v.jy[NL] - gy));
-            }
-            if (q_part) {
-#pragma unroll
-              for (int d = 1; d < NL; ++d) {
-                double sn, cs;
-                fgx_sincos(v.q[d], &sn, &cs);
-                st_row(so, row_of(k, d), N, e4, (float)cs);
-                st_row(so, row_of(k, NL + d), N, e4, (float)sn);
-              }
-            }
           } else {
-            if (fk_part) {
-              st_row(so, row_of(k, 0), N, e4, fnan);
-              st_row(so, row_of(k, NL), N, e4, fnan);
-              st_row(so, row_of(k, 3 * NL), N, e4, fnan);
-              st_row(so, row_of(k, 3 * NL + 1), N, e4, fnan);
-            }
-            if (q_part) {
 #pragma unroll
-              for (int d = 1; d < NL; ++d) {
-                st_row(so, row_of(k, d), N, e4, fnan);
-                st_row(so, row_of(k, NL + d), N, e4, fnan);
-              }
-            }
+            for (int p = 0; p < 2 * NL; ++p) st_row(so, row_of(k, p), N, e4, fnan);
+            st_row(so, row_of(k, 3 * NL), N, e4, fnan);
+            st_row(so, row_of(k, 3 * NL + 1), N, e4, fnan);
           }
         }
       }
       __syncthreads();   // chunk it - 1 read; chunk it staged
     }
+    rets[pair * 64 + lane] = ps.result(L, split);
+    __syncthreads();   // the returns staged
     return;
   }
 
@@ -226,11 +173,6 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
     }
     tg.init(c, params + e * c.n_params, tab, s0, ic_q, ic_qd);
   }
-  const int L = sg.L;
-  // numpy pairwise split of the return sum (SimpleReacher never terminates: L is known now)
-  const int split = (L > 128) ? ((L / 2) & ~7) : 0;
-  PairwiseSum ps;
-  ps.init();
   bool trunc = false;
   const double act_lo = __builtin_canonicalize(c.act_lo), act_hi = __builtin_canonicalize(c.act_hi);
   // (every info store is a typed global store, st_row: a generic pointer would make it a FLAT store,
@@ -241,25 +183,6 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
   auto row = [&](int k, int b, int i) __attribute__((always_inline)) {
     float pos[NL], vel[NL];
     tg.at(c, k, pos, vel);
-#ifdef FGX_V2_ABL_DYNST   // A/B builds only: the dynamics waves store no per-sample rows
-    if (valid && k < L) {
-      double a[NL];
-      float a32[NL];
-#pragma unroll
-      for (int d = 0; d < NL; ++d) {
-        const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
-        const double cl = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
-        a[d] = (u != u) ? u : cl;
-        a32[d] = 0.0f;
-      }
-      const StepOut r = substep<ENV_SIMPLE, false, NL, true>(c, v, a, a32, false);
-      trunc = v.steps >= c.max_steps;
-      ps.add(k, r.reward, split);
-#pragma unroll
-      for (int d = 0; d < NL; ++d) rq(b, i, d) = v.q[d];
-    }
-    return;
-#endif
     if (!valid) return;
     if (oo.positions) {
 #pragma unroll
@@ -281,7 +204,7 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
       }
       const StepOut r = substep<ENV_SIMPLE, false, NL, true>(c, v, a, a32, false);
       trunc = v.steps >= c.max_steps;
-      ps.add(k, r.reward, split);
+      rq(b, i, NL) = r.reward;   // (the observation waves sum the return)
       if (oo.step_actions)
 #pragma unroll
         for (int d = 0; d < NL; ++d) st_row(oo.step_actions, (int64_t)k * NL + d, N, e8, a[d]);
@@ -331,10 +254,11 @@ __global__ __launch_bounds__(kV2Threads) void k_episode_v2(DevCfg c, DevState s,
     }
     __syncthreads();   // chunk it staged; chunk it - 1 read
   }
+  __syncthreads();   // the returns staged
   if (!valid) return;
   // the epilogue needs FK of the final q; a last sample at env step >= 199 has just computed it
   if (!(v.steps - 1 >= 199)) v.fk();
-  episode_epilogue(c, s, o, e, v, sg.plans, L, ps.result(L, split), false, trunc);
+  episode_epilogue(c, s, o, e, v, sg.plans, L, rets[pair * 64 + lane], false, trunc);
 }
 
 }  // namespace fgx
