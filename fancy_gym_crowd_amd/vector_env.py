@@ -244,8 +244,9 @@ class BlackBoxVectorEnv:
         obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
         fobs = torch.empty_like(obs)
         ret = torch.empty(N, dtype=torch.float64, device=self.device)
-        te = torch.empty(N, dtype=torch.uint8, device=self.device)
-        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        # (bool tensors: the library writes bytes 0 / 1, so .bool() below is free, no conversion kernel)
+        te = torch.empty(N, dtype=torch.bool, device=self.device)
+        tr = torch.empty(N, dtype=torch.bool, device=self.device)
         tl = torch.empty(N, dtype=torch.int32, device=self.device)
         info_s, bufs = self._info_buffers()
         _lib.check(self._eng.lib.fgx_step(self._eng.h, _ptr(a), _ptr(obs), _ptr(ret), _ptr(te), _ptr(tr), _ptr(tl),
@@ -264,8 +265,9 @@ class BlackBoxVectorEnv:
         obs = torch.empty((N, self.out_dim), dtype=torch.float32, device=self.device)
         fobs = torch.empty_like(obs)
         ret = torch.empty(N, dtype=torch.float64, device=self.device)
-        te = torch.empty(N, dtype=torch.uint8, device=self.device)
-        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        # (bool tensors: the library writes bytes 0 / 1, so .bool() below is free, no conversion kernel)
+        te = torch.empty(N, dtype=torch.bool, device=self.device)
+        tr = torch.empty(N, dtype=torch.bool, device=self.device)
         tl = torch.empty(N, dtype=torch.int32, device=self.device)
         info_s, bufs = self._info_buffers()
         _lib.check(self._eng.lib.fgx_step_traj(self._eng.h, _ptr(p), _ptr(v), _ptr(obs), _ptr(ret), _ptr(te),
@@ -431,8 +433,9 @@ class StepVectorEnv:
         obs = torch.empty((N, self.obs_dim), dtype=torch.float32, device=self.device)
         fobs = torch.empty_like(obs)
         rew = torch.empty(N, dtype=torch.float64, device=self.device)
-        te = torch.empty(N, dtype=torch.uint8, device=self.device)
-        tr = torch.empty(N, dtype=torch.uint8, device=self.device)
+        # (bool tensors: the library writes bytes 0 / 1, so .bool() below is free, no conversion kernel)
+        te = torch.empty(N, dtype=torch.bool, device=self.device)
+        tr = torch.empty(N, dtype=torch.bool, device=self.device)
         _lib.check(self._eng.lib.fgx_step_raw(self._eng.h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(te), _ptr(tr),
                                               _ptr(fobs), int(self.autoreset), self._eng.stream()))
         term, trunc = te.bool(), tr.bool()

@@ -20,4 +20,8 @@ cut -c1-400 gpurun_out/r04f_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04f_rocprof -o bench -- \
   python3 bench.py --no-cpu-baseline > gpurun_out/r04f_rocprof.log 2>&1 || exit $?
 echo "rocprof ok"
+# the verbose-2 step's kernels (k_episode_v2 and what else a public step() launches)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04f_rocprof_log -o log -- \
+  python3 tools/bench_kernels.py logsimple levels > gpurun_out/r04f_rocprof_log.log 2>&1 || exit $?
+echo "rocprof log ok"
 exit $rc
