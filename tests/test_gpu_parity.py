@@ -624,6 +624,29 @@ def test_trajectory_mfma_equals_valu(env_id, N, monkeypatch):
             np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+@pytest.mark.parametrize("env_id,N,duration", [("fancy_ProMP/SimpleReacher-v0", 1000, 2.56),
+                                               ("fancy_ProDMP/SimpleReacher-v0", 777, 2.56),
+                                               ("fancy_ProMP/SimpleReacher-v0", 96, 2.28),
+                                               ("fancy_ProDMP/SimpleReacher-v0", 64, 2.4)])
+def test_trajectory_mfma_long_plans(env_id, N, duration, monkeypatch):
+    """k_traj_mfma at the engine's longest plans (T <= 256): ProMP T = 256 is 9 tiles, two segments of
+    the workgroup's 8 waves; T = 228 one segment whose last tile outputs 32 rows; ProDMP T = 256 / 240
+    8 tiles.  Against k_traj_valu, bit for bit."""
+    outs = []
+    for replan in (None, int(round(duration / 0.01))):
+        over = {"black_box_kwargs": {"duration": duration}}
+        if replan:
+            over["black_box_kwargs"]["replanning_schedule"] = fgx.ReplanEvery(replan)
+        env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+        assert env.T == int(round(duration / 0.01))
+        params = torch.from_numpy(np.random.default_rng(9).standard_normal((N, env.n_params), dtype=np.float32)).to(DEV)
+        env.reset(seed=3)
+        outs.append([np_(x) for x in env.trajectory(params)])
+    for a, b in zip(outs[0], outs[1]):
+        assert a.shape == b.shape
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.mark.parametrize("env_id,over", [
     ("fancy_ProDMP/HoleReacher-v0", {"basis_generator_kwargs": {"dt": 0.005}}),
     ("fancy_ProDMP/SimpleReacher-v0", {"basis_generator_kwargs": {"dt": 0.02}}),
