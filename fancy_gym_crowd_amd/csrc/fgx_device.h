@@ -168,6 +168,15 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// workgroup barrier for an LDS handover between waves: this wave's LDS operations complete, then
+// s_barrier; unlike __syncthreads no fence on global memory, so outstanding global stores are not
+// waited for (vmcnt) — the storing waves keep their stores in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ------------------------------------------------------------------ wave write-combining of info rows
 // The logging k_episode writes the verbose-2 per-step arrays ([T, N] / [T, X, N], up to GBs per BB
 // step).  InfoStage collects the wave's values of one sample (every row of every array) in the wave's
@@ -211,14 +220,20 @@ struct InfoStage {
   bool plan_rows;  // positions / velocities are this kernel's (not a given plan)
 
   // region: the block's staging area (after the basis table); e: the lane's env (< N)
-  __device__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan) {
-    lane = (int)(threadIdx.x & 63);
-    full_dim = c.full_dim;
-    n32 = stage_n32(NL, c.full_dim);
-    char* w = region + (size_t)(threadIdx.x >> 6) * stage_wave_bytes(NL, c.full_dim);
+  __device__ __forceinline__ void init(const DevCfg& c, const Outputs& o, char* region, int64_t e, bool plan) {
+    init_at(c, o, region + (size_t)(threadIdx.x >> 6) * stage_wave_bytes(NL, c.full_dim), e, plan);
+  }
+  // the staging slot at w (k_episode_v2h: two slots per dynamics wave, flushed by a partner wave)
+  __device__ __forceinline__ void rebase(char* w) {
     d = (double*)w;
     f = (float*)(w + N64 * 512);
     b = (uint8_t*)(w + N64 * 512 + n32 * 256);
+  }
+  __device__ __forceinline__ void init_at(const DevCfg& c, const Outputs& o, char* w, int64_t e, bool plan) {
+    lane = (int)(threadIdx.x & 63);
+    full_dim = c.full_dim;
+    n32 = stage_n32(NL, c.full_dim);
+    rebase(w);
     N = c.N;
     e0 = e - lane;
     nval = (int)min((int64_t)64, N - e0);
@@ -269,7 +284,7 @@ struct InfoStage {
   }
 
   // write the staged rows of sample kk (wave-uniform); every lane of the wave's envs active
-  __device__ void flush(int kk, const Outputs& o) {
+  __device__ __forceinline__ void flush(int kk, const Outputs& o) {
     if (!any) return;
     wave_lds_sync();
     const uint32_t k = (uint32_t)kk;

@@ -69,7 +69,7 @@ namespace fgx {
 //    its exchange rows stopped conflicting on LDS banks).
 // k_episode_jp and k_episode_ws stay selectable: FGX_EPISODE_KERNEL=classic|jp|ws|jl forces a kernel
 // wherever it applies (A/B benchmarks, tests).
-enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_PAIR = 5, EK_V2 = 6 };
+enum : int { EK_CLASSIC = 0, EK_JP = 1, EK_WS = 2, EK_JL = 3, EK_CLASSIC_W2 = 4, EK_PAIR = 5, EK_V2 = 6, EK_V2H = 7 };
 
 inline int64_t round_envs() {   // envs of one k_episode round: one 64-lane wave per SIMD
   static const int64_t r = [] {
@@ -91,7 +91,20 @@ inline bool w2_applies(const DevCfg& c, bool log) { return c.env == ENV_SIMPLE &
 // pairs' second wave per SIMD does not pay for the duplicated plan / controller / dynamics work
 // (65536: 648 vs 530 us; profiles/r03_pair_scan.jsonl).  FGX_EPISODE_KERNEL=classic / =pair force.
 inline bool pair_applies(const DevCfg& c, bool log) { return c.env == ENV_HOLE && c.nl == 5 && !log; }
+// k_episode_v2h (fgx_kernels.h): the per-step info rows of the direct envs (HoleReacher,
+// ViaPointReacher) stored by a partner wave per SIMD; whole 256-env workgroups only.  FGX_V2=0 (or
+// FGX_EPISODE_KERNEL=classic) keeps the logging k_episode (A/B, tests)
+inline bool v2h_applies(const DevCfg& c, bool log) {
+  if (const char* v = std::getenv("FGX_V2"))
+    if (std::strcmp(v, "0") == 0) return false;
+  if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))
+    if (std::strcmp(v, "classic") == 0) return false;
+  return log && c.env != ENV_SIMPLE && c.N % 256 == 0 && (c.nl == 2 || c.nl == 5) &&
+         v2h_lds_bytes(c.mp, c.rows, c.stride, c.nl, c.full_dim) <= 160 * 1024;
+}
+
 inline int classic_choice(const DevCfg& c, bool log) {
+  if (v2h_applies(c, log)) return EK_V2H;
   if (pair_applies(c, log)) {
     if (const char* v = std::getenv("FGX_EPISODE_KERNEL")) {
       if (std::strcmp(v, "classic") == 0) return EK_CLASSIC;
@@ -236,6 +249,21 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
                          s, params, dpos, dvel, o);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) { err = std::string("k_episode_w2 launch: ") + hipGetErrorString(e); return -2; }
+      return 0;
+    }
+  }
+  if constexpr (!LOG_ONLY && ENV != ENV_SIMPLE) {
+    if (v2h_applies(c, log)) {
+      const size_t lh = v2h_lds_bytes(MP, c.rows, c.stride, NL, c.full_dim);
+      if (lh > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_v2h<ENV, MP, CTRL, NL, NB>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lh) != hipSuccess) {
+        err = "k_episode_v2h: cannot raise the dynamic LDS limit";
+        return -2;
+      }
+      hipLaunchKernelGGL((k_episode_v2h<ENV, MP, CTRL, NL, NB>), dim3((unsigned)(c.N / 256)), dim3(512), lh, stream,
+                         c, s, params, dpos, dvel, o);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) { err = std::string("k_episode_v2h launch: ") + hipGetErrorString(e); return -2; }
       return 0;
     }
   }

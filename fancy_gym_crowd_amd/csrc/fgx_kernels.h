@@ -27,10 +27,12 @@ namespace fgx {
 // gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
 // s1: element stride of d1 (the per-step observations: the lane's column of the wave's LDS staging
 // slots, stride 64, InfoStage)
+// skip_q: cos / sin of q[1..NL) are left as 0 placeholders (k_episode_v2h: the storing wave writes
+// them, from the staged q, before the row leaves)
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
                                          bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
-                                         const double* gsn = nullptr, int s1 = 1) {
+                                         const double* gsn = nullptr, int s1 = 1, bool skip_q = false) {
   const bool rs = !ctx || c.random_start;
   int p = 0;
   auto put = [&](float x) {
@@ -50,6 +52,7 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
       for (int k = 0; k < NL; ++k) {
         if (gcs) { cs[k] = gcs[k]; sn[k] = gsn[k]; }
         else if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
+        else if (skip_q) { cs[k] = 0.0; sn[k] = 0.0; }
         else fgx_sincos(v.q[k], &sn[k], &cs[k]);
       }
     }
@@ -751,18 +754,22 @@ __device__ inline void invalid_transition(const DevCfg& c, const DevState& s, co
 // PAIR (k_episode_pair): two lanes per env (lanes 2i, 2i + 1 hold env i), both running the whole
 // step; the FK sincos and the collision tests are divided between them (Env::fk_pair).  Every store
 // is made by both lanes with the same value; the inner-step counter takes the even lanes' lengths.
-template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG, bool PAIR = false>
+// HELPED (k_episode_v2h): the logging body of waves 0..3 of a 512-thread workgroup whose waves 4..7
+// store the per-step rows; the table is staged by the kernel, each sample's rows go to one of two
+// staging slots per wave and one LDS-only workgroup barrier per sample hands them over.
+template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG, bool PAIR = false, bool HELPED = false>
 __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s, const float* __restrict__ params,
                                              const float* __restrict__ dpos, const float* __restrict__ dvel,
                                              const Outputs& o) {
   static_assert(!(PAIR && (LOG || ENV == ENV_SIMPLE)), "lane pairs serve the direct envs without per-step info");
+  static_assert(!HELPED || (LOG && !PAIR), "the helped body is the logging one");
   extern __shared__ float lds_tab[];
-  if (MP != MP_GIVEN) {
+  if (MP != MP_GIVEN && !HELPED) {
     const int n = c.rows * c.stride;
     for (int i = threadIdx.x; i < n; i += blockDim.x) lds_tab[i] = s.tables[i];
     __syncthreads();
   }
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * (HELPED ? 256 : blockDim.x) + threadIdx.x;
   const int64_t e = PAIR ? (tid >> 1) : tid;
   const int pp = PAIR ? (int)(threadIdx.x & 1) : 0;
   if (e >= c.N) return;
@@ -803,10 +810,28 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   // The wave walks the rows together (lanes whose env has stopped pad their row beside the running
   // ones) and the staged rows of each sample leave the wave as wide stores (InfoStage::flush).
   InfoStage<NL> ist;
+  char* helped_slots = nullptr;   // HELPED: this wave's two staging slots
+  int row = 0;                    // HELPED: rows handed over so far
   if constexpr (LOG) {
     const size_t tabf = (MP == MP_GIVEN) ? 0 : (size_t)c.rows * c.stride;
-    ist.init(c, o, (char*)lds_tab + stage_tab_offset(tabf), e, MP != MP_GIVEN);
+    if constexpr (HELPED) {
+      helped_slots = (char*)lds_tab + stage_tab_offset(tabf) +
+                     (size_t)(2 * (threadIdx.x >> 6)) * stage_wave_bytes(NL, c.full_dim);
+      ist.init_at(c, o, helped_slots, e, MP != MP_GIVEN);
+    } else {
+      ist.init(c, o, (char*)lds_tab + stage_tab_offset(tabf), e, MP != MP_GIVEN);
+    }
   }
+  // the staged rows of sample kk leave: as this wave's wide stores, or (HELPED) to the partner wave
+  auto emit_row = [&](int kk) __attribute__((always_inline)) {
+    if constexpr (HELPED) {
+      lds_barrier();
+      ++row;
+      ist.rebase(helped_slots + (size_t)(row & 1) * stage_wave_bytes(NL, c.full_dim));
+    } else {
+      ist.flush(kk, o);
+    }
+  };
   auto pad_row = [&](int kk, auto& gen) {
     const double dnan = __builtin_nan("");
     const float fnan = __builtin_nanf("");
@@ -821,6 +846,9 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     ist.rew(dnan);
     float* so = ist.obs_row();
     for (int q = 0; q < c.full_dim; ++q) so[q * 64] = fnan;
+    if constexpr (HELPED)   // (a NaN q: the storing wave leaves the padding's NaN)
+#pragma unroll
+      for (int d = 1; d < NL; ++d) ist.ql(d, dnan);
     ist.flags(0, 0);
     ist.ee(dnan, dnan);
     ist.rdc(dnan, dnan);
@@ -939,7 +967,10 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
         if (c.time_aware) so[(3 * NL + 3) * 64] = (float)((double)v.steps / (double)c.max_steps);
       } else if (o.step_obs) {
         // (FK is current after every logged sample: fk_always; cos / sin of q[0] are FK's)
-        emit_obs(c, v, false, ist.obs_row(), nullptr, false, true, nullptr, nullptr, 64);
+        emit_obs(c, v, false, ist.obs_row(), nullptr, false, true, nullptr, nullptr, 64, HELPED);
+        if constexpr (HELPED)   // cos / sin of q[1..]: the storing wave's (k_episode_v2h)
+#pragma unroll
+          for (int d = 1; d < NL; ++d) ist.ql(d, v.q[d]);
       }
       if (ENV != ENV_SIMPLE) {
         ist.flags((uint8_t)r.coll, (uint8_t)r.success);
@@ -1203,13 +1234,14 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
         L = min(L, k);
         if (k < c.T) pad_row(k, tg);
       }
-      if (k < c.T) ist.flush(__builtin_amdgcn_readfirstlane(k), o);
+      if (k < c.T) emit_row(__builtin_amdgcn_readfirstlane(k));
     }
     L = min(L, k);
     for (int kk = __builtin_amdgcn_readfirstlane(k); kk < c.T; ++kk) {
       pad_row(kk, tg);
-      ist.flush(kk, o);
+      emit_row(kk);
     }
+    if constexpr (HELPED) lds_barrier();   // the partner has stored the last row
     if (invalid) {
       invalid_transition(c, s, o, e, v);
       return;
@@ -1252,6 +1284,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     DevCfg c, DevState s, const float* __restrict__ params, const float* __restrict__ dpos,
     const float* __restrict__ dvel, Outputs o) {
   episode_body<ENV, MP, CTRL, NL, NB, false, true>(c, s, params, dpos, dvel, o);
+}
+
+// k_episode_v2h: the verbose-2 step of the direct envs (HoleReacher, ViaPointReacher).  The logging
+// k_episode runs one lone wave per SIMD that computes a sample and then stores its ~30 info rows;
+// here waves 0..3 run the same logging body (episode_body HELPED) and hand each sample's staged rows
+// to waves 4..7 (wave w + 4 shares wave w's SIMD), which issue the stores (InfoStage::flush, the same
+// code and the same bytes), so the dynamics wave never issues a global info store; the storing wave
+// also computes the observation's cos / sin of q[1..NL) from the staged q (emit_obs skip_q: the
+// same fgx_sincos on the same q; q[0]'s are FK's, computed for the dynamics anyway).  Two staging
+// slots per dynamics wave, one LDS-only barrier per sample (s_barrier after lgkmcnt(0): a
+// __syncthreads fence would make the storing waves wait for their own stores every sample).  The
+// grid covers N with whole workgroups (N % 256 == 0, fgx_dispatch.h): every wave meets every barrier.
+template <int ENV, int MP, int CTRL, int NL, int NB>
+__global__ __launch_bounds__(512) void k_episode_v2h(DevCfg c, DevState s, const float* __restrict__ params,
+                                                     const float* __restrict__ dpos, const float* __restrict__ dvel,
+                                                     Outputs o) {
+  extern __shared__ float lds_tab[];
+  const int tabn = (MP != MP_GIVEN) ? c.rows * c.stride : 0;
+  for (int i = threadIdx.x; i < tabn; i += blockDim.x) lds_tab[i] = s.tables[i];
+  __syncthreads();   // table staged
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w < 4) {
+    episode_body<ENV, MP, CTRL, NL, NB, true, false, true>(c, s, params, dpos, dvel, o);
+    return;
+  }
+  // the storing wave of dynamics wave w - 4: row k from slot k & 1, after the barrier that follows it
+  const int pw = w - 4;
+  const size_t wb = stage_wave_bytes(NL, c.full_dim);
+  char* slots = (char*)lds_tab + stage_tab_offset((size_t)tabn) + (size_t)(2 * pw) * wb;
+  InfoStage<NL> ist;
+  ist.init_at(c, o, slots, (int64_t)blockIdx.x * 256 + pw * 64 + (threadIdx.x & 63), MP != MP_GIVEN);
+  const int lane = threadIdx.x & 63;
+  for (int k = 0; k < c.T; ++k) {
+    lds_barrier();
+    ist.rebase(slots + (size_t)(k & 1) * wb);
+    if (o.step_obs) {
+      // the observation's cos / sin of q[1..NL) (emit_obs's fgx_sincos on the staged q; a NaN q is a
+      // padded row: its NaN stays)
+      float* so = ist.obs_row();
+#pragma unroll
+      for (int d = 1; d < NL; ++d) {
+        const double q = ist.d[(NL + 5 + d) * 64 + lane];
+        if (q == q) {
+          double sn, cs;
+          fgx_sincos(q, &sn, &cs);
+          so[d * 64] = (float)cs;
+          so[(NL + d) * 64] = (float)sn;
+        }
+      }
+    }
+    ist.flush(k, o);
+  }
+  lds_barrier();
+}
+
+inline size_t v2h_lds_bytes(int mp, int rows, int stride, int nl, int full_dim) {
+  const size_t tabf = (mp == MP_GIVEN) ? 0 : (size_t)rows * stride;
+  return stage_tab_offset(tabf) + 8 * stage_wave_bytes(nl, full_dim);
 }
 
 template <int ENV, int MP, int CTRL, int NL, int NB, bool LOG>

@@ -44,8 +44,10 @@ def _rows(dev, ref, L, name, T):
 def test_info_rows_vs_oracle(ci, N):
     env_id, over = CASES[ci]
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
-    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher: the logging k_episode
-    assert env.episode_kernel(info_level=2) == ("k_episode" if "Hole" in env_id else "k_episode_v2")
+    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher: k_episode_v2h at whole 256-env
+    # workgroups, else the logging k_episode
+    want = ("k_episode_v2h" if N % 256 == 0 else "k_episode") if "Hole" in env_id else "k_episode_v2"
+    assert env.episode_kernel(info_level=2) == want
     spec = spec_of(env)
     tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
     ob = batched.BatchedBB(NAME[env_id.split("/")[1]], N, ctrl_of(env), mp_spec=spec, info_level=2, tables=tabs,
@@ -174,3 +176,49 @@ def test_v2_observation_fallback_lanes(env_id, monkeypatch):
     np.testing.assert_array_equal(np_(ra[0]), np_(rb[0]))
     np.testing.assert_array_equal(np_(ra[4]["step_observations"]), np_(rb[4]["step_observations"]))
     assert np.isfinite(np_(ra[4]["step_observations"])[:, :10]).all()
+
+
+V2H_CASES = [
+    ("fancy_ProDMP/HoleReacher-v0", None, {}),
+    ("fancy_DMP/HoleReacher-v0", None, {}),
+    ("fancy_ProMP/HoleReacher-v0", None, {"allow_self_collision": True}),
+    ("fancy_ProDMP/HoleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(50)}}, {}),
+    ("fancy_ProMP/ViaPointReacher-v0", None, {}),
+    ("fancy_DMP/HoleReacher-v0", None, {"n_links": 2}),
+]
+
+
+@pytest.mark.parametrize("N", [512, 1024])
+@pytest.mark.parametrize("info_level", [1, 2])
+@pytest.mark.parametrize("ci", range(len(V2H_CASES)))
+def test_v2h_equals_logging_kernel(ci, info_level, N, monkeypatch):
+    """k_episode_v2h (fgx_kernels.h: the logging body on waves 0..3, its per-step rows stored by waves
+    4..7) against the logging k_episode (FGX_V2=0): every per-step array, the step outputs and the
+    whole device state bit for bit over 6 BB steps with collisions (terminations at every sample),
+    auto-resets and replanning segments."""
+    env_id, over, kw = V2H_CASES[ci]
+    a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    assert a.episode_kernel() == "k_episode_v2h"
+    np.testing.assert_array_equal(np_(a.reset(seed=5)[0]), np_(b.reset(seed=5)[0]))
+    rng = np.random.default_rng(ci + 10 * info_level)
+    lengths = set()
+    for _ in range(6):
+        p = torch.from_numpy((rng.standard_normal((N, a.n_params)) * 3).astype(np.float32)).to(DEV)
+        monkeypatch.delenv("FGX_V2", raising=False)
+        ra = a.step(p)
+        monkeypatch.setenv("FGX_V2", "0")
+        rb = b.step(p)
+        monkeypatch.delenv("FGX_V2")
+        for x, y in zip(ra[:4], rb[:4]):
+            np.testing.assert_array_equal(np_(x), np_(y))
+        keys = [k for k in ra[4] if isinstance(ra[4][k], torch.Tensor) and not k.startswith("_")]
+        assert "is_collided" in keys and (info_level < 2 or "step_observations" in keys)
+        for k in keys:
+            np.testing.assert_array_equal(np_(ra[4][k]), np_(rb[4][k]), err_msg=k)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)
+        lengths |= set(np_(ra[4]["trajectory_length"]).tolist())
+    if "Hole" in env_id:
+        assert len(lengths) > 2   # collisions ended episodes at different samples
