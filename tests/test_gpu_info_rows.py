@@ -222,3 +222,42 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, monkeypatch):
         lengths |= set(np_(ra[4]["trajectory_length"]).tolist())
     if "Hole" in env_id:
         assert len(lengths) > 2   # collisions ended episodes at different samples
+
+
+@pytest.mark.parametrize("mode", ["step_trajectory", "validity"])
+def test_v2h_given_plans_and_validity(mode, monkeypatch):
+    """k_episode_v2h on the other logging paths: caller-supplied plans (fgx_step_traj, MP_GIVEN: no
+    basis table, the rows from the given arrays) and trajectory-validity checks (invalid plans pad
+    every row, then the artificial transition after the last barrier); bit for bit against the
+    logging k_episode."""
+    N = 512
+    env_id = "fancy_ProDMP/HoleReacher-v0"
+    kw = {}
+    if mode == "validity":
+        kw["traj_validity"] = fgx.TrajValidity(pos_low=[-1.2] * 5, pos_high=[1.2] * 5, invalid_return=-3.0,
+                                               terminated=True, truncated=False, obs="current")
+    a = fgx.make(env_id, num_envs=N, device=DEV, **kw)
+    b = fgx.make(env_id, num_envs=N, device=DEV, **kw)
+    assert a.episode_kernel() == "k_episode_v2h"
+    np.testing.assert_array_equal(np_(a.reset(seed=2)[0]), np_(b.reset(seed=2)[0]))
+    rng = np.random.default_rng(12)
+    for _ in range(4):
+        p = torch.from_numpy((rng.standard_normal((N, a.n_params)) * 2).astype(np.float32)).to(DEV)
+        if mode == "step_trajectory":
+            pos, vel = a.trajectory(p)
+            pos = pos + torch.from_numpy(rng.standard_normal(pos.shape).astype(np.float32) * 0.05).to(DEV)
+        monkeypatch.delenv("FGX_V2", raising=False)
+        ra = a.step_trajectory(pos, vel) if mode == "step_trajectory" else a.step(p)
+        monkeypatch.setenv("FGX_V2", "0")
+        rb = b.step_trajectory(pos, vel) if mode == "step_trajectory" else b.step(p)
+        monkeypatch.delenv("FGX_V2")
+        for x, y in zip(ra[:4], rb[:4]):
+            np.testing.assert_array_equal(np_(x), np_(y))
+        for k in [k for k in ra[4] if isinstance(ra[4][k], torch.Tensor) and not k.startswith("_")]:
+            np.testing.assert_array_equal(np_(ra[4][k]), np_(rb[4][k]), err_msg=k)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)
+    if mode == "validity":
+        tl = np_(ra[4]["trajectory_length"])
+        assert (tl == 0).any() and (tl > 0).any()   # both valid and invalid plans took part
