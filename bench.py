@@ -101,11 +101,41 @@ def env_id_of(env):
     return env.meta["env_id"]
 
 
+def basis_gemm_fields(N, T, n, nb, n_params, t, pmc):
+    """The basis GEMM's accounting from its launch time t (s) and its committed PMC entry (or None).
+    Algorithmic work: ONE contraction per env, plan = table [T, nb] x weights [nb, dof] (ProMP: the
+    velocities are a forward difference of the positions, no second GEMM), 2 nb T dof flops per env.
+    What the matrix cores issue is the MFMA-padded count (K = 8 for nb = 5, 8 tiles of 28 rows for
+    T = 200): SQ_INSTS_VALU_MFMA_MOPS_F32 of the PMC pass.  mfma_frac = those issued flops over the
+    launch time, against the f32 matrix peak."""
+    flops = 2 * nb * T * n * N
+    out_bytes = 2 * 4 * N * T * n + 4 * N * n_params
+    out = {"flops_algorithmic": flops, "us": t * 1e6, "algorithmic_tflops": flops / t / 1e12,
+           "peak_tflops": FP32_VEC_PEAK_TF, "hbm_GBps": out_bytes / t / 1e9,
+           "hbm_frac": out_bytes / t / 1e9 / HBM_PEAK_GBS, "pmc": None}
+    if pmc is not None and pmc.get("mfma_f32_flops"):
+        issued = float(pmc["mfma_f32_flops"])
+        out["pmc"] = {"mfma_f32_instr": pmc.get("mfma_f32_instr"), "mfma_f32_flops_issued": issued,
+                      "mfma_busy_cycles": pmc.get("mfma_busy_cycles"),
+                      "issued_over_algorithmic": issued / flops,
+                      "traffic_bytes_per_launch": pmc.get("traffic_bytes_per_launch"),
+                      "kernel_ns_under_pmc": (pmc.get("kernel_ns_median_under_pmc") or {}).get("mfma"),
+                      "source": pmc.get("source")}
+        out["mfma_tflops"] = issued / t / 1e12
+        out["mfma_frac"] = issued / t / 1e12 / FP32_VEC_PEAK_TF
+        out["mfma_frac_source"] = "PMC-issued MFMA flops of this build / launch time"
+    else:   # no PMC pass of this build: the algorithmic count (a lower bound of what is issued)
+        out["mfma_tflops"] = flops / t / 1e12
+        out["mfma_frac"] = flops / t / 1e12 / FP32_VEC_PEAK_TF
+        out["mfma_frac_source"] = "algorithmic flops / launch time (no PMC pass of this build)"
+    return out
+
+
 def basis_gemm(env, params, reps=10):
     """The MP basis x weights contraction as its own launch (BlackBoxWrapper.get_trajectory ->
     fgx_trajectory -> k_traj_mfma, v_mfma_f32_32x32x2_f32 with K = 8): time per launch from HIP
     events around a graph replay of `reps` launches, MFMA utilisation against the f32 matrix peak
-    and the HBM rate of its [N, T, dof] f32 outputs."""
+    (basis_gemm_fields) and the HBM rate of its [N, T, dof] f32 outputs."""
     import ctypes
 
     import torch
@@ -127,25 +157,12 @@ def basis_gemm(env, params, reps=10):
     e1.record()
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / reps * 1e-3
-    flops = 2 * 2 * 8 * N * n * T                 # two K = 8 GEMMs (positions, next positions)
-    out_bytes = 2 * 4 * N * T * n + 4 * N * env.n_params
     pmc, note = pmc_entry(env_id_of(env), N, "k_traj_mfma", lib_build_id())
-    counters = None
-    if pmc is not None and pmc.get("mfma_f32_flops"):
-        ns = (pmc.get("kernel_ns_median_under_pmc") or {}).get("mfma")
-        counters = {"mfma_f32_instr": pmc.get("mfma_f32_instr"), "mfma_f32_flops": pmc["mfma_f32_flops"],
-                    "mfma_busy_cycles": pmc.get("mfma_busy_cycles"),
-                    "pmc_flops_over_algorithmic": pmc["mfma_f32_flops"] / flops,
-                    "traffic_bytes_per_launch": pmc.get("traffic_bytes_per_launch"),
-                    "kernel_ns_under_pmc": ns, "source": pmc.get("source")}
-        if ns:
-            counters["pmc_mfma_frac"] = pmc["mfma_f32_flops"] / (ns * 1e-9) / 1e12 / FP32_VEC_PEAK_TF
-    return {"kernel": "k_traj_mfma", "us": t * 1e6, "mfma_tflops": flops / t / 1e12, "pmc": counters,
-            "pmc_note": note,
-            "peak_tflops": FP32_VEC_PEAK_TF, "mfma_frac": flops / t / 1e12 / FP32_VEC_PEAK_TF,
-            "hbm_GBps": out_bytes / t / 1e9, "hbm_frac": out_bytes / t / 1e9 / HBM_PEAK_GBS,
-            "note": "K = 8 (5 basis + zero pad): arithmetic intensity 2 flop/B, bound by the output "
-                    "write; the fused episode kernels evaluate the same contraction in registers instead"}
+    out = {"kernel": "k_traj_mfma", "pmc_note": note}
+    out.update(basis_gemm_fields(N, T, n, env._eng.cfg.n_basis, env.n_params, t, pmc))
+    out["note"] = ("K = 8 (5 basis + zero pad): arithmetic intensity 2 flop/B, bound by the output write; the fused "
+                   "episode kernels evaluate the same contraction in registers instead")
+    return out
 
 
 # ----------------------------------------------------------------------------- CPU baseline

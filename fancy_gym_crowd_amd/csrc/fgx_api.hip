@@ -282,7 +282,12 @@ static int build_devcfg(const fgx_config& c, int64_t N, DevCfg& d, int& ctx_dim)
   d.alpha_phase = c.alpha_phase;
   d.bandwidth = c.bandwidth;
   d.bdt = c.basis_dt > 0.0 ? c.basis_dt : c.dt;
-  if (c.mp_kind == FGX_MP_PRODMP && prodmp_fine_rows(d.dt, d.bdt, d.rows, d.tau, d.delay) > (1 << 20))
+  // the fine grid's extent: row i looks up rint(max(t_i - delay, 0) / bdt), largest for the smallest
+  // delay -- with learn_delay each env's own clipped delay (>= delay_bound_lo, the per-env walk of
+  // prodmp_rows_seq), else the static one
+  if (c.mp_kind == FGX_MP_PRODMP &&
+      prodmp_fine_rows(d.dt, d.bdt, d.rows, d.tau, c.learn_delay ? std::min(d.delay, c.delay_bound_lo) : d.delay) >
+          (1 << 20))
     return fail(FGX_E_UNSUPPORTED, "ProDMP precompute grid too fine (basis dt far below the env dt)");
   if (c.n_gains != 0 && c.n_gains != c.n_links)   // p_gains * (des_pos - c_pos) must broadcast
     return fail(FGX_E_INVALID, "per-joint PD gains must have n_links entries");

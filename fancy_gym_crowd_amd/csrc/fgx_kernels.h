@@ -27,8 +27,9 @@ namespace fgx {
 // gcs / gsn (optional): cos / sin of every q[k], computed elsewhere with the same sincos
 // s1: element stride of d1 (the per-step observations: the lane's column of the wave's LDS staging
 // slots, stride 64, InfoStage)
-// skip_q: cos / sin of q[1..NL) are left as 0 placeholders (k_episode_v2h: the storing wave writes
-// them, from the staged q, before the row leaves)
+// skip_q: cos / sin of q[1..NL) are left as NaN placeholders (k_episode_v2h: the storing wave writes
+// them, from the staged q, before the row leaves; it skips a NaN q, whose cos / sin are NaN anyway --
+// a padded row, or a running env whose state went NaN through NaN parameters)
 template <int NL>
 __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool ctx, float* d1, float* d2,
                                          bool fresh = false, bool fk0 = false, const double* gcs = nullptr,
@@ -52,7 +53,7 @@ __device__ __forceinline__ void emit_obs(const DevCfg& c, const Env<NL>& v, bool
       for (int k = 0; k < NL; ++k) {
         if (gcs) { cs[k] = gcs[k]; sn[k] = gsn[k]; }
         else if (k == 0 && fk0) { cs[0] = v.c[0]; sn[0] = v.s[0]; }   // FK's first angle is q[0]
-        else if (skip_q) { cs[k] = 0.0; sn[k] = 0.0; }
+        else if (skip_q) { cs[k] = __builtin_nan(""); sn[k] = __builtin_nan(""); }
         else fgx_sincos(v.q[k], &sn[k], &cs[k]);
       }
     }
@@ -1320,8 +1321,8 @@ __global__ __launch_bounds__(512) void k_episode_v2h(DevCfg c, DevState s, const
     lds_barrier();
     ist.rebase(slots + (size_t)(k & 1) * wb);
     if (o.step_obs) {
-      // the observation's cos / sin of q[1..NL) (emit_obs's fgx_sincos on the staged q; a NaN q is a
-      // padded row: its NaN stays)
+      // the observation's cos / sin of q[1..NL) (emit_obs's fgx_sincos on the staged q; for a NaN q --
+      // a padded row, or a running env with NaN state -- the NaN placeholder stays, as sincos(NaN))
       float* so = ist.obs_row();
 #pragma unroll
       for (int d = 1; d < NL; ++d) {

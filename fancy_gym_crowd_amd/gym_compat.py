@@ -62,15 +62,20 @@ class SingleEnv:
         self._env.close()
 
 
-def gym_spaces(env_id, gym_module, **env_kwargs):
+def _to_gym_box(b, gym_module):
+    """the engine's Box stand-in as a `gym_module.spaces.Box` (same low / high / shape / dtype)"""
+    return gym_module.spaces.Box(low=b.low, high=b.high, shape=b.shape, dtype=b.dtype)
+
+
+def gym_spaces(env_id, gym_module, mp_config_override=None, **env_kwargs):
     """(observation_space, action_space) of one env of `env_id` as `gym_module.spaces.Box` instances
     (same low / high / shape / dtype as the engine's own Box stand-in), from the resolved config
     alone (no device work).  gymnasium's env checker requires spaces derived from gymnasium.spaces.Space."""
     from .registry import resolve
     from .vector_env import action_space, observation_space
-    cfg, meta = resolve(env_id, None, **env_kwargs)
-    conv = lambda b: gym_module.spaces.Box(low=b.low, high=b.high, shape=b.shape, dtype=b.dtype)   # noqa: E731
-    return conv(observation_space(cfg)), conv(action_space(cfg, meta.get("n_params", 0)))
+    cfg, meta = resolve(env_id, mp_config_override, **env_kwargs)
+    return (_to_gym_box(observation_space(cfg), gym_module),
+            _to_gym_box(action_space(cfg, meta.get("n_params", 0)), gym_module))
 
 
 def registered_ids():
@@ -88,9 +93,13 @@ def register_gymnasium(device="cuda:0", gym_module=None):
         except ImportError:
             return False
     def _init(self, env_id, device="cuda:0", **kwargs):
+        # every make() kwarg (mp_config_override, info_level, env kwargs, ...) goes to the engine once,
+        # as bb_env_constructor takes them (envs/registry.py:280-309)
         SingleEnv.__init__(self, env_id, device, **kwargs)
-        # gymnasium's PassiveEnvChecker rejects spaces that are not gymnasium.spaces.Space instances
-        self.observation_space, self.action_space = gym_spaces(env_id, gym, **kwargs)
+        # gymnasium's PassiveEnvChecker rejects spaces that are not gymnasium.spaces.Space instances:
+        # the spaces of the env just built, converted (never a second resolve of the kwargs)
+        self.observation_space = _to_gym_box(self.observation_space, gym)
+        self.action_space = _to_gym_box(self.action_space, gym)
 
     base = type("GymSingleEnv", (SingleEnv, gym.Env), {"__init__": _init})
     for env_id in registered_ids():

@@ -78,3 +78,31 @@ def test_pmc_summary_rebuilds_from_committed_csvs(tmp_path):
         for fld in ("valu_instr_per_launch", "traffic_bytes_per_launch"):
             if fld in e:
                 assert g[key(e)][fld] == e[fld]
+
+
+def test_basis_gemm_accounting_from_pmc():
+    """bench.py's basis-GEMM fields: ONE contraction per env is the algorithmic work (2 nb T dof N
+    flops: ProMP's velocities are a forward difference, not a second GEMM), the PMC pass counts the
+    MFMA-padded flops actually issued (K = 8 for 5 basis functions, 8 tiles of 28 rows for T = 200),
+    and mfma_frac = issued flops / launch time / f32 matrix peak (round 4: 0.067, not 0.119)."""
+    with open(bench.PMC_SUMMARY) as f:
+        entries = json.load(f)["entries"]
+    pmc = [e for e in entries if e["kernel"] == "k_traj_mfma" and int(e["envs"]) == 65536
+           and e["workload"] == "fancy_ProMP/LongSimpleReacher-v0"]
+    assert pmc
+    pmc = pmc[0]
+    N, T, n, nb = 65536, 200, 5, 5
+    t = pmc["kernel_ns_median_under_pmc"]["mfma"] * 1e-9
+    f = bench.basis_gemm_fields(N, T, n, nb, n * nb, t, pmc)
+    assert f["flops_algorithmic"] == 2 * nb * T * n * N
+    # issued = padded: K 8 / 5 and 224 rows / 200 (ProMP tiles of 28 of 32 rows)
+    assert f["pmc"]["issued_over_algorithmic"] == pytest.approx(8 / 5 * 224 / 200, rel=1e-9)
+    assert f["mfma_frac"] == pytest.approx(pmc["mfma_f32_flops"] / t / 1e12 / bench.FP32_VEC_PEAK_TF, rel=1e-12)
+    assert 0.05 < f["mfma_frac"] < 0.09
+    assert f["algorithmic_tflops"] < f["mfma_tflops"]
+    line = _line()
+    bg = line.get("basis_gemm", {})
+    if "flops_algorithmic" in bg and bg.get("pmc"):   # a bench line of the corrected accounting
+        g = bench.basis_gemm_fields(N, T, n, nb, n * nb, bg["us"] * 1e-6, pmc)
+        for k in ("flops_algorithmic", "mfma_frac", "algorithmic_tflops", "hbm_GBps"):
+            assert g[k] == pytest.approx(bg[k], rel=1e-9), k

@@ -224,6 +224,54 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, monkeypatch):
         assert len(lengths) > 2   # collisions ended episodes at different samples
 
 
+@pytest.mark.parametrize("env_id,over", [("fancy_ProDMP/HoleReacher-v0", None),
+                                         ("fancy_ProMP/ViaPointReacher-v0",
+                                          {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}})])
+def test_v2h_nonfinite_lanes(env_id, over, monkeypatch):
+    """k_episode_v2h with NaN / inf parameters and NaN / huge joint angles mixed into ordinary waves:
+    a NaN action passes np.clip, NaN positions never collide, so those envs keep running with NaN
+    state and their observation rows carry NaN cos / sin (the storing wave's placeholder, as sincos(NaN)
+    in the logging kernel); bit for bit against the logging k_episode (FGX_V2=0).  Also a grid larger
+    than one round of workgroups (N = 66048) and ViaPointReacher with a replanning schedule."""
+    for N in (768, 66048):
+        a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+        b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
+        assert a.episode_kernel() == "k_episode_v2h"
+        a.reset(seed=9)
+        b.reset(seed=9)
+        rng = np.random.default_rng(N)
+        if N == 768:
+            st = a.get_state()
+            q = np_(st["q"]).copy()
+            q[5:N:23, 1] = np.nan
+            q[9:N:29, 2] = 1e7
+            for e in (a, b):
+                e.set_state(q=q)
+        for it in range(3):
+            p = (rng.standard_normal((N, a.n_params)) * 2).astype(np.float32)
+            p[it::7] = np.nan
+            p[3 + it::11, 2] = np.inf
+            p[4::13, 0] = -np.inf
+            p = torch.from_numpy(p).to(DEV)
+            monkeypatch.delenv("FGX_V2", raising=False)
+            ra = a.step(p)
+            monkeypatch.setenv("FGX_V2", "0")
+            rb = b.step(p)
+            monkeypatch.delenv("FGX_V2")
+            for x, y in zip(ra[:4], rb[:4]):
+                np.testing.assert_array_equal(np_(x), np_(y))
+            for k in [k for k in ra[4] if isinstance(ra[4][k], torch.Tensor) and not k.startswith("_")]:
+                np.testing.assert_array_equal(np_(ra[4][k]), np_(rb[4][k]), err_msg=k)
+            sa, sb = a.get_state(), b.get_state()
+            for k in sa:
+                np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)
+        if N == 768:   # some NaN-parameter envs ran to the end with NaN rows
+            so = np_(ra[4]["step_observations"])
+            L = np_(ra[4]["trajectory_length"])
+            assert (np.isnan(so[it::7, 0, 1]) & (L[it::7] > 1)).any()
+        del a, b
+
+
 @pytest.mark.parametrize("mode", ["step_trajectory", "validity"])
 def test_v2h_given_plans_and_validity(mode, monkeypatch):
     """k_episode_v2h on the other logging paths: caller-supplied plans (fgx_step_traj, MP_GIVEN: no

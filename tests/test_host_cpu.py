@@ -252,6 +252,39 @@ def test_register_gymnasium_with_stand_in():
         assert fgx.register_gymnasium() is False
 
 
+def test_gym_make_entry_point_forwards_kwargs(monkeypatch):
+    """gym.make(id, mp_config_override=..., info_level=..., **env_kwargs) through the registered entry
+    point: every kwarg reaches the engine once (bb_env_constructor, envs/registry.py:280-309) and the
+    gymnasium spaces are the built env's own, converted (so an override that changes the parameter
+    count changes the action space)."""
+    import types
+    from fancy_gym_crowd_amd import gym_compat
+    from fancy_gym_crowd_amd.vector_env import Box, action_space, observation_space
+    made = []
+
+    def fake_make(env_id, num_envs=1, device="cuda", mp_config_override=None, info_level=None, autoreset=True,
+                  **env_kwargs):
+        cfg, meta = fgx.resolve(env_id, mp_config_override, **env_kwargs)
+        made.append(dict(env_id=env_id, override=mp_config_override, info_level=info_level, env_kwargs=env_kwargs))
+        n = meta.get("n_params", 0)
+        return types.SimpleNamespace(n_params=n, single_observation_space=observation_space(cfg),
+                                     single_action_space=Box(-np.inf, np.inf, (n,), np.float32)
+                                     if meta["mp_type"] else action_space(cfg, n))
+
+    monkeypatch.setattr(fgx, "make", fake_make)
+    calls = []
+    stand_in = types.SimpleNamespace(Env=object, register=lambda **kw: calls.append(kw), spaces=_StandInSpaces)
+    assert fgx.register_gymnasium(gym_module=stand_in) is True
+    entry = {c["id"]: c["entry_point"] for c in calls}
+    over = {"basis_generator_kwargs": {"num_basis": 7}}
+    env = entry["fancy_ProMP/LongSimpleReacher-v0"](mp_config_override=over, info_level=1, seed_offset=0)
+    assert made[-1]["override"] == over and made[-1]["info_level"] == 1
+    assert isinstance(env.action_space, _StandInSpaces.Space) and env.action_space.shape == (35,)
+    assert isinstance(env.observation_space, _StandInSpaces.Space) and env.observation_space.shape == (17,)
+    env = entry["fancy/HoleReacher-v0"](n_links=3)
+    assert made[-1]["env_kwargs"] == {"n_links": 3} and env.action_space.shape == (3,)
+
+
 def test_num_basis_outside_resolution():
     """basis_generator_kwargs num_basis_outside (mp_pytorch NormalizedRBF / ProDMP generators)."""
     c, _ = fgx.resolve("fancy_DMP/SimpleReacher-v0", {"basis_generator_kwargs": {"num_basis_outside": 1}})

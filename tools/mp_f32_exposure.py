@@ -1,0 +1,218 @@
+"""How much do the engine's outcomes depend on the oracle's unpinned table arithmetic?
+
+The basis tables (phase, normalized RBF, ProDMP variation-of-parameters integrals) are what
+mp_pytorch (<=0.1.3, not in this container) computes in **torch float32** on the CPU (SURVEY.md
+Appendix A).  The oracle and the device compute every table value in f64 and round once to f32
+(oracle/mp.py).  This script rebuilds the same tables with every operation in torch float32 —
+mp_pytorch's arithmetic, restated (its exact operation order stays unpinned) — and runs the oracle
+(oracle/batched.py, TEST INFRASTRUCTURE) on both table sets over the same seeds and parameters:
+
+  * config 3: fancy_ProDMP/HoleReacher-v0, 65536 envs, 2 BB steps (collisions: flags and lengths
+    carry information);
+  * the metric: fancy_ProMP/LongSimpleReacher-v0, 65536 envs, 2 BB steps.
+
+It counts terminated / truncated / trajectory_length flips and the largest observation and return
+deviations.  Output: one JSON object (stdout, and --out).  Reference call sites of the tables:
+black_box_wrapper.py:119-133 (set params / initial conditions / duration, get_traj_pos / vel).
+
+Usage: python tools/mp_f32_exposure.py [--envs 65536] [--steps 2] [--workers 8] [--out FILE]
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import multiprocessing as mproc
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from oracle import batched, mp  # noqa: E402
+
+CONFIGS = {
+    "config3": ("fancy_ProDMP/HoleReacher-v0", "HoleReacher"),
+    "metric": ("fancy_ProMP/LongSimpleReacher-v0", "LongSimpleReacher"),
+}
+
+
+def spec_from_cfg(c):
+    """oracle MPSpec of a resolved C config (fancy_gym_crowd_amd.resolve; no device)"""
+    kind = {1: "promp", 2: "dmp", 3: "prodmp"}[c.mp_kind]
+    return mp.MPSpec(kind=kind, dof=c.n_links, n_basis=c.n_basis, phase="linear" if c.phase_kind == 0 else "exp",
+                     tau=c.tau, delay=c.delay, alpha_phase=c.alpha_phase, bandwidth=c.bandwidth,
+                     zero_start=c.zero_start, zero_goal=c.zero_goal, basis_outside=c.num_basis_outside,
+                     weights_scale=c.weights_scale, goal_scale=c.goal_scale, alpha=c.alpha, pc_length=c.pc_length,
+                     dt=c.dt, duration=c.duration, basis_dt=c.basis_dt if c.mp_kind == 3 else 0.0)
+
+
+# ----------------------------------------------------------------------------- torch float32 tables
+def _t32(torch, x):
+    return torch.as_tensor(np.asarray(x), dtype=torch.float32)
+
+
+def phase32(torch, spec, t):
+    lin = torch.clamp((t - np.float32(spec.delay)) / np.float32(spec.tau), min=0.0)
+    if spec.phase == "linear":
+        return torch.clamp(lin, max=1.0)
+    return torch.exp(np.float32(-spec.alpha_phase) * lin)
+
+
+def rbf32(torch, spec, x):
+    n = spec.n_basis + spec.zero_start + spec.zero_goal
+    o = spec.basis_outside
+    u = (torch.arange(n, dtype=torch.float32) - o) / np.float32(n - 2 * o - 1) if n > 1 else torch.zeros(1)
+    c = u if spec.phase == "linear" else torch.exp(np.float32(-spec.alpha_phase) * u)
+    if n > 1:
+        d = torch.empty(n, dtype=torch.float32)
+        d[:-1] = c[1:] - c[:-1]
+        d[-1] = d[-2]
+    else:
+        d = torch.ones(1)
+    h = np.float32(spec.bandwidth) / (d * d)
+    dd = x[..., None] - c
+    e = torch.exp(-h * dd * dd / 2)
+    phi = e / e.sum(-1, keepdim=True)
+    return phi[..., spec.zero_start:spec.zero_start + spec.n_basis]
+
+
+def build_tables32(spec, n_rows):
+    """oracle/mp.py:build_tables with every operation in torch float32"""
+    import torch
+    i = torch.arange(n_rows + 1, dtype=torch.float32)
+    t = i * np.float32(spec.dt)
+    if spec.kind == "promp":
+        phi = np.float32(spec.weights_scale) * rbf32(torch, spec, phase32(torch, spec, t[:n_rows]))
+        return dict(phi=phi.numpy().astype(np.float32), dt32=(t[1:] - t[:-1]).numpy().astype(np.float32))
+    if spec.kind == "dmp":
+        x = phase32(torch, spec, t[:n_rows])
+        psi = x[:, None] * rbf32(torch, spec, x)
+        s = torch.clamp((t - np.float32(spec.delay)) / np.float32(spec.tau), min=0.0)
+        return dict(psi=psi.numpy(), sdt=(s[1:] - s[:-1]).numpy())
+    assert spec.kind == "prodmp"
+    assert not spec.delay and spec.bdt == spec.dt, "the configs measured here have no delay / own basis dt"
+    h = np.float32(spec.bdt / spec.tau)
+    J = max(int(round(spec.pc_length / float(h))) + 1, n_rows)
+    s = torch.arange(J, dtype=torch.float32) * h
+    a = np.float32(spec.alpha)
+    x = torch.exp(np.float32(-spec.alpha_phase) * s)
+    phi = rbf32(torch, spec, x)
+    e = torch.exp(a * s / 2)
+    dp1 = (s * e * x)[:, None] * phi
+    dp2 = (e * x)[:, None] * phi
+    z = torch.zeros(1, phi.shape[1])
+    p1 = torch.cat([z, torch.cumsum(h * (dp1[:-1] + dp1[1:]) / 2, 0)], 0)   # cumulative trapezoid, f32
+    p2 = torch.cat([z, torch.cumsum(h * (dp2[:-1] + dp2[1:]) / 2, 0)], 0)
+    y1 = torch.exp(-a * s / 2)
+    y2 = s * y1
+    dy1 = -a / 2 * y1
+    dy2 = -a / 2 * y2 + y1
+    q1 = (a * s / 2 - 1) * e + 1
+    q2 = a / 2 * (e - 1)
+    pb = torch.cat([p2 * y2[:, None] - p1 * y1[:, None], (q2 * y2 - q1 * y1)[:, None]], 1)
+    vb = torch.cat([p2 * dy2[:, None] - p1 * dy1[:, None], (q2 * dy2 - q1 * dy1)[:, None]], 1)
+    out = dict(pb=pb, vb=vb, y1=y1, y2=y2, dy1=dy1, dy2=dy2)
+    return {k: v[:n_rows].numpy().astype(np.float32) for k, v in out.items()}
+
+
+def table_deviation(t64, t32):
+    """largest |f32 table - f64-then-round table| per entry kind, relative to the entry kind's max |value|,
+    and the share of entries that differ"""
+    out = {}
+    for k in t64:
+        a, b = np.asarray(t64[k], np.float64), np.asarray(t32[k], np.float64)
+        scale = max(np.abs(a).max(), 1e-300)
+        out[k] = dict(max_rel_to_max=float(np.abs(a - b).max() / scale), frac_differ=float((a != b).mean()))
+    return out
+
+
+# ----------------------------------------------------------------------------- oracle runs
+def run_chunk(args):
+    """flags, lengths, returns and observations of global envs [lo, hi) (env i seeded i)"""
+    name, ctrl, spec, tables, kw, lo, hi, plist = args
+    ob = batched.BatchedBB(name, hi - lo, ctrl, mp_spec=spec, tables=tables, **kw)
+    ob._reset_idx(list(range(hi - lo)), list(range(lo, hi)))
+    out = []
+    for p in plist:
+        obs, ret, te, tr, info = ob.step(p)
+        out.append((info["trajectory_length"], te, tr, ret, obs, info["final_obs"]))
+    return lo, out
+
+
+def run_oracle(name, ctrl, spec, tables, kw, plist, N, workers, chunks):
+    step = N // chunks
+    jobs = [(name, ctrl, spec, tables, kw, lo, lo + step, [p[lo:lo + step] for p in plist]) for lo in range(0, N, step)]
+    if workers > 1:
+        with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mproc.get_context("spawn")) as ex:
+            res = dict(ex.map(run_chunk, jobs))
+    else:
+        res = dict(map(run_chunk, jobs))
+    return [tuple(np.concatenate([res[lo][b][f] for lo in sorted(res)]) for f in range(6)) for b in range(len(plist))]
+
+
+def exposure(cfg_name, N, n_bb, workers=8, chunks=16):
+    import fancy_gym_crowd_amd as fgx
+    env_id, name = CONFIGS[cfg_name]
+    c, meta = fgx.resolve(env_id)
+    spec = spec_from_cfg(c)
+    ctrl = ("pd", c.p_gain, c.d_gain) if c.ctrl_kind == 0 else {1: ("vel",), 2: ("pos",)}[c.ctrl_kind]
+    kw = dict(replan_period=c.replan_period, condition_on_desired=bool(c.condition_on_desired))
+    rows = spec.T + 2
+    t64 = mp.build_tables(spec, rows)
+    t32 = build_tables32(spec, rows)
+    rng = np.random.default_rng(1234)   # SURVEY §8(d) synthetic parameters
+    plist = [rng.standard_normal((N, spec.n_params), dtype=np.float32) for _ in range(n_bb)]
+    t0 = time.time()
+    a = run_oracle(name, ctrl, spec, t64, kw, plist, N, workers, chunks)
+    b = run_oracle(name, ctrl, spec, t32, kw, plist, N, workers, chunks)
+    steps = []
+    for s in range(n_bb):
+        la, ta, ra, reta, oa, fa = a[s]
+        lb, tb, rb, retb, obb, fb = b[s]
+        fin = np.isfinite(reta) & np.isfinite(retb)
+        rel = np.abs(reta[fin] - retb[fin]) / np.maximum(np.abs(reta[fin]), 1e-300)
+        same_len = la == lb
+        relsame = rel[same_len[fin]]
+        steps.append(dict(
+            bb_step=s,
+            length_flips=int((la != lb).sum()),
+            terminated_flips=int((ta != tb).sum()),
+            truncated_flips=int((ra != rb).sum()),
+            terminated_count=int(ta.sum()),
+            mean_length=float(la.mean()),
+            max_return_rel_dev=float(rel.max()) if rel.size else 0.0,
+            max_return_rel_dev_same_length=float(relsame.max()) if relsame.size else 0.0,
+            returns_beyond_1e5_rel=int((rel > 1e-5).sum()),
+            max_obs_abs_dev=float(np.nanmax(np.abs(fa.astype(np.float64) - fb.astype(np.float64)))),
+            # outside the parity tests' observation tolerance (rtol 1e-5, atol 1e-6, tests/test_gpu_parity.py)
+            obs_outside_tol=int((np.abs(fa.astype(np.float64) - fb.astype(np.float64)) >
+                                 1e-5 * np.abs(fa.astype(np.float64)) + 1e-6).sum()),
+            obs_values=int(fa.size),
+        ))
+    return dict(config=cfg_name, env_id=env_id, envs=N, bb_steps=n_bb, tables=table_deviation(t64, t32),
+                steps=steps, seconds=round(time.time() - t0, 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--configs", default="config3,metric")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = dict(what="outcome exposure to the unpinned MP table arithmetic: torch float32 tables (mp_pytorch's "
+                    "arithmetic, restated) vs the oracle's f64-then-round tables, same seeds / parameters",
+               results=[exposure(n, a.envs, a.steps, a.workers) for n in a.configs.split(",")])
+    s = json.dumps(res, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
