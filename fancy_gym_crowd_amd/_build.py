@@ -24,7 +24,7 @@ STAMP = LIB + ".buildid"
 OBJDIR = os.path.join(HERE, "csrc", "build")
 # (the longest units first: the pool starts them before the short ones)
 SOURCES = ["fgx_ep_hole_gen.hip", "fgx_ep_hole.hip", "fgx_ep_simple_gen.hip", "fgx_ep_simple.hip",
-           "fgx_ep_via_gen.hip", "fgx_ep_via.hip", "fgx_ep_jl.hip"] + \
+           "fgx_ep_via_gen.hip", "fgx_ep_via.hip", "fgx_ep_jl.hip", "fgx_ep_hp.hip"] + \
           [f"fgx_ep_nl{n}.hip" for n in (1, 3, 4, 6, 7, 8)] + ["fgx_api.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          # numerics: every expression rounds like the numpy reference; fmas only where written

@@ -85,7 +85,8 @@ EXPORTS = {
     "fgx_selftest_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 EPISODE_KERNELS = {0: "k_episode", 1: "k_episode_jp", 2: "k_episode_ws", 3: "k_episode_jl", 4: "k_episode_w2",
-                   5: "k_episode_pair", 6: "k_episode_v2", 7: "k_episode_v2h"}
+                   5: "k_episode_pair", 6: "k_episode_v2", 7: "k_episode_v2h",
+                   8: "k_episode_hp"}
 
 _LIB = None
 

@@ -17,6 +17,7 @@
 #include "fgx_dispatch.h"
 #include "fgx_learned.h"
 #include "fgx_step.h"
+#include "fgx_hp.h"
 
 using namespace fgx;
 
@@ -78,9 +79,18 @@ static const NlOps* nl_ops(int nl) {
   return nullptr;
 }
 
+// any per-step output, or the validity checks: the logging instantiations (fgx_dispatch.h)
+static bool episode_logs(const DevCfg& c, const Outputs& o) {
+  return o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector ||
+         o.reward_dist || c.valid_flags != 0;
+}
+
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
   if (const NlOps* ops = nl_ops(h.dc.nl)) return ops->episode(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
+  // HoleReacher without per-step info: the producer / consumer pipeline (fgx_hp.h)
+  if (hp_applies(h.dc, h.st, mp, episode_logs(h.dc, o), h.st.plan_len != nullptr))
+    return fgx_launch_episode_hp(h.dc, h.st, mp, params, o, stream, g_err);
   const bool gen = mp != MP_GIVEN && h.dc.nb != 5;   // generic basis-count instantiations
   if (h.dc.env == ENV_SIMPLE)
     return (gen ? fgx_launch_episode_simple_gen : fgx_launch_episode_simple)(h.dc, h.st, mp, params, dpos, dvel, o,
@@ -392,10 +402,12 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_start = off; off = align_up(off + sizeof(double) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
   const size_t o_tabt = off; off = align_up(off + sizeof(float) * (size_t)tables_t_rows(h->dc.rows) * h->dc.stride);
-  // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128)
-  const bool need_rew = (cfg->env_kind != FGX_ENV_SIMPLE || h->dc.sched_state) && cfg->mp_kind != FGX_MP_NONE &&
-                        h->dc.T > 128;
-  const size_t o_rew = off; off = align_up(off + (need_rew ? sizeof(double) * (size_t)h->dc.T * N : 0));
+  // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128, k_episode);
+  // for the direct envs also k_episode_hp's candidate final states (2 (2 n_links + 1) rows, fgx_hp.h)
+  const bool direct = cfg->env_kind != FGX_ENV_SIMPLE && cfg->mp_kind != FGX_MP_NONE;
+  const bool need_rew = direct || (h->dc.sched_state && cfg->mp_kind != FGX_MP_NONE && h->dc.T > 128);
+  const size_t rew_rows = direct ? (size_t)std::max(h->dc.T, 2 * (2 * nl + 1)) : (size_t)h->dc.T;
+  const size_t o_rew = off; off = align_up(off + (need_rew ? sizeof(double) * rew_rows * N : 0));
   e = hipMalloc(&h->state_block, off);
   if (e != hipSuccess) { delete h; return fail(FGX_E_NOMEM, std::string("hipMalloc state: ") + hipGetErrorString(e)); }
   char* b = (char*)h->state_block;
@@ -720,7 +732,10 @@ int fgx_episode_kernel(void* handle, int32_t info_level) {
   if (!h) return fail(FGX_E_INVALID, "null handle");
   const int mp = h->learned() ? MP_GIVEN : h->dc.mp;
   // the predicate launch_episode_nl uses: any per-step output, or the validity checks
-  return episode_kernel_choice(h->dc, mp, info_level >= 1 || h->dc.valid_flags != 0, h->learned());
+  const bool log = info_level >= 1 || h->dc.valid_flags != 0;
+  if (h->dc.nl == 2 || h->dc.nl == 5)
+    if (hp_applies(h->dc, h->st, mp, log, h->learned())) return EK_HP;
+  return episode_kernel_choice(h->dc, mp, log, h->learned());
 }
 
 }  // extern "C"

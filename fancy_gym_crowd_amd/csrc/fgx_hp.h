@@ -1,0 +1,418 @@
+// fgx_hp.h — k_episode_hp: the HoleReacher black-box step as a producer / consumer pipeline.
+//
+// BlackBoxWrapper.step (black_box_wrapper.py:170-253) over HoleReacher (hole_reacher.py:73-179,
+// hr_simple_reward.py:19-53, base_reacher_direct.py:20-38): per plan sample the tracking controller,
+// np.clip, the direct-velocity Euler step (q̇ = a, q += dt q̇), FK, the self- and wall-collision tests
+// and the reward; the episode segment ends at the first collision.  The dynamics never read the
+// collision result (the controller reads q and q̇ only, base_reacher_direct.py:25-27,
+// black_box_wrapper.py:202-205): collisions only end the episode and enter the reward.  So the sample
+// stream splits exactly, without rollback, into
+//   * a producer wave P (one env per lane, as k_episode): plan, controller, clip, Σ acc², Euler — the
+//     f64 chain that depends on the previous sample; it writes q and acc_cost of every sample (and the
+//     action, the final q̇ candidate) into an LDS ring, chunk by chunk, running up to one chunk ahead;
+//   * two consumer waves C0 / C1 on the same 64 envs: C_i takes the samples k ≡ i (mod 2) of each
+//     two-sample chunk: FK, self / wall collision, the reward (hr_simple_reward) — the independent,
+//     costly part (≈ 3/4 of k_episode's instructions);
+//   * the resolution, one chunk later on both consumers (identically): the first sample that collides
+//     or reaches the static end (plan end, TimeLimit, replanning sample) ends the segment; every
+//     earlier sample counts.
+// The return is numpy's pairwise sum (umath pairwise_sum) of the counted rewards, computed online
+// although the length L is only known at the end: pairwise slot j = k & 7 is owned by consumer
+// j & 1 (= k & 1), which keeps its four slots' accumulators of committed full 8-blocks for the
+// level-1 sum (L <= 128) and for every second-half start s = (L/2) & ~7 that an L in (128, 200] can
+// give (64, 72, 80, 88, 96); the partial last block's rewards stay in a 16-deep LDS ring until the
+// end, and block(0, s) is formed by an LDS exchange when the first s samples have been counted.  The
+// sum's rounding sequence is numpy's for every L (== PairwiseSum / pairwise_strided).  No [T][N]
+// reward scratch in HBM.
+//
+// Workgroups of G groups (3 G waves, 64 envs per group): waves 0..G-1 are the producers, G..2G-1
+// the consumers C0, 2G..3G-1 the consumers C1 of group w % G; with G = 4 the three waves of a group
+// share one SIMD (wave w runs on SIMD w % 4, profiles/r01_wave_placement.txt), one workgroup per CU.
+// One LDS-only barrier per two-sample chunk.  The producer reads the basis rows from global memory
+// (all lanes the same row: one broadcast request per wave), so LDS holds only the rings.
+//
+// Served (hp_applies): HoleReacher with the simple reward function, 5 links, 5 basis functions per
+// joint, shared tables (no learned tau / delay), static replanning schedules, no
+// condition_on_desired, no validity checks, no per-step info, max_episode_steps <= 200.  Every output
+// and the whole env state equal k_episode's bit for bit (tests/test_gpu_hp.py).
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "fgx_kernels.h"
+
+namespace fgx {
+
+constexpr int EK_HP = 8;   // fgx_episode_kernel's id (include/fgx.h)
+constexpr int kHpNS = 5;   // second-half starts s = 64, 72, ..., 96 of numpy's split for L in (128, 200]
+constexpr int kHpS0 = 64;
+constexpr int kHpNR = 2;   // of them in the producer's registers (64, 72); the rest in LDS
+constexpr int kHpPA = 10;  // depth of the producer's acc_cost ring (its lead over the resolution + 8)
+// candidate final state rows per consumer in the handle's direct-env scratch: q, q̇, |ee - goal|^2
+template <int NL> __host__ __device__ constexpr int hp_cand_rows() { return 2 * NL + 1; }
+
+// LDS of one group (doubles): the q ring [buf][i][d][lane] and the action ring [buf][i][d][lane] (the
+// consumers' input: chunk it in buffer it & 1), the consumers' stop codes [buf][i][lane] (u8), the
+// producer's acc_cost ring [k % 10][lane],
+// the second-half accumulators of the LDS-held split starts [s][slot][lane], block(0, s) [s][lane]
+// and the alive masks [parity] (u64)
+template <int NL>
+struct HpLayout {
+  static constexpr int RQ = 2 * 2 * NL * 64;
+  static constexpr int RA = 2 * 2 * NL * 64;
+  static constexpr int RS = 2 * 2 * 64 / 8;
+  static constexpr int PA = kHpPA * 64;
+  static constexpr int BL = (kHpNS - kHpNR) * 8 * 64;
+  static constexpr int FF = kHpNS * 64;
+  static constexpr int AL = 2;
+  static constexpr int GROUP = RQ + RA + RS + PA + BL + FF + AL;
+  static constexpr int oRQ = 0, oRA = RQ, oRS = oRA + RA, oPA = oRS + RS, oBL = oPA + PA,
+                       oFF = oBL + BL, oAL = oFF + FF;
+};
+
+template <int MP, int CTRL, int NL, int NB, int G>
+__global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, const float* __restrict__ params,
+                                                       Outputs o) {
+  using Lay = HpLayout<NL>;
+  constexpr bool F32 = (CTRL != CTRL_PD);
+  extern __shared__ double lds_hp[];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int g = w % G, role = w / G;   // role 0: producer, 1: consumer C0, 2: consumer C1
+  double* gr = lds_hp + (size_t)g * Lay::GROUP;
+  uint64_t* al = (uint64_t*)(gr + Lay::oAL);
+  uint8_t* rs = (uint8_t*)(gr + Lay::oRS);
+  const int64_t N = c.N;
+  const int64_t e0 = (int64_t)blockIdx.x * (64 * G) + g * 64 + lane;
+  const bool valid = e0 < N;
+  const int64_t e = valid ? e0 : N - 1;   // clamped: loads stay in bounds, nothing is stored
+  const int T = c.T;
+  double* cand = s.rew;   // candidate final states [ci][q | q̇ | |ee - goal|^2][N] (the handle's direct-env scratch)
+  constexpr int CR = hp_cand_rows<NL>();
+
+  // ---- every role: the env's static segment end (black_box_wrapper.py:233-239: plan end, TimeLimit,
+  // replanning sample); a collision can only end it earlier
+  const int steps0 = s.steps[e];
+  const int plans = s.plans[e] + 1;
+  const bool plans_ok = c.replan && (c.max_plans <= 0 || plans < c.max_plans);
+  const int k_replan = plans_ok ? first_static_replan(c, steps0) : -1;
+  int Lst = min(T, max(1, c.max_steps - steps0));
+  if (k_replan >= 0) Lst = min(Lst, k_replan + 1);
+  const int itmax = (T + 1) / 2 + 3;
+  {
+    const uint64_t vm = __ballot(valid);
+    if (role == 0 && lane == 0) al[1] = vm;   // read as "iteration -1" by iteration 0
+  }
+  __syncthreads();
+  auto all_done = [&](int rp) __attribute__((always_inline)) {
+    uint64_t any = 0;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) any |= ((const uint64_t*)(lds_hp + (size_t)gg * Lay::GROUP + Lay::oAL))[rp];
+    return any == 0;
+  };
+
+  if (role != 0) {
+    // ================================================================ consumers
+    const int ci = role - 1;   // sample k = 2 c + ci of chunk c
+    const double gx = s.goal[e], gy = s.goal[N + e];
+    // the wall's edges (Env::wall_collision: left / right of the hole, its depth below the ground)
+    const double hx = s.hole[e], hw = s.hole[N + e], hd = s.hole[2 * N + e];
+    const double w_left = hx - hw / 2, w_right = hx + hw / 2, w_nd = -hd;
+    const bool allow_self = c.allow_self != 0, allow_wall = c.allow_wall != 0;
+    bool own_done = false;   // this consumer saw a stop sample of the env: the segment ends there or earlier
+    for (int it = 0;; ++it) {
+      const int rp = (it + 1) & 1;
+      if (all_done(rp) || it > itmax) break;
+      const int cpk = it - 1;
+      const int k = 2 * cpk + ci;
+      const bool alive = ((al[rp] >> lane) & 1) && !own_done;
+      if (it >= 1 && alive && k < Lst) {
+        const double* rq = gr + Lay::oRQ + (size_t)((cpk & 1) * 2 + ci) * NL * 64;
+        // FK (base_reacher.py:95-103, Env::fk's operations) fused with the wall test of each link as
+        // soon as its start joint and direction exist (hole_reacher.py:126-179, Env::wall_collision's
+        // per-link test): only the joint positions stay live for the self-collision test
+        // (base_reacher.py:105-119); q is read from the ring as it is needed
+        double jx[NL + 1], jy[NL + 1];
+        jx[0] = 0.0; jy[0] = 0.0;
+        bool lim = false, wc = false;
+        double ang = 0.0, x = 0.0, y = 0.0;
+#pragma unroll
+        for (int d = 0; d < NL; ++d) {
+          const double qv = rq[d * 64 + lane];
+          lim |= qv > M_PI || qv < -M_PI;   // base_reacher.py:38-39,111
+          ang = (d == 0) ? qv : ang + qv;
+          double sn, cs;
+          fgx_sincos(ang, &sn, &cs);
+          x = (d == 0) ? cs : x + cs;
+          y = (d == 0) ? sn : y + sn;
+          jx[d + 1] = 0.0 + x;
+          jy[d + 1] = 0.0 + y;
+          if (!allow_wall && !(jy[d] >= 0.0 && jy[d + 1] >= 0.0 && w_nd <= 0.0))
+            wc |= Env<NL>::link_wall(w_left, w_right, w_nd, jx[d], jy[d], cs, sn);
+        }
+        bool sc = false;
+        if (!allow_self) {
+          sc = lim;
+#pragma unroll
+          for (int i = 0; i < NL; ++i)
+#pragma unroll
+            for (int j = i + 2; j < NL; ++j)
+              sc |= (ccw(jx[i], jy[i], jx[j], jy[j], jx[j + 1], jy[j + 1]) !=
+                     ccw(jx[i + 1], jy[i + 1], jx[j], jy[j], jx[j + 1], jy[j + 1])) &&
+                    (ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j], jy[j]) !=
+                     ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j + 1], jy[j + 1]));
+        }
+        const bool coll = sc || wc;   // hr_simple_reward.py:19-53
+        const bool stop = coll || k == Lst - 1;
+        rs[((cpk & 1) * 2 + ci) * 64 + lane] = (uint8_t)((stop ? 1 : 0) | (coll ? 2 : 0));
+        if (stop) {
+          // a candidate final state: this sample ends the segment unless an earlier one does; with the
+          // distance term of the reward at a collision or at env step 199 (hr_simple_reward.py:33-45)
+          const double* ra = gr + Lay::oRA + (size_t)((cpk & 1) * 2 + ci) * NL * 64;
+          double* cd = cand + (int64_t)(ci * CR) * N + e;
+#pragma unroll
+          for (int d = 0; d < NL; ++d) {
+            cd[(int64_t)d * N] = rq[d * 64 + lane];
+            cd[(int64_t)(NL + d) * N] = ra[d * 64 + lane];
+          }
+          const double dist = norm2(jx[NL] - gx, jy[NL] - gy);
+          cd[(int64_t)(2 * NL) * N] = dist * dist;
+          own_done = true;
+        }
+      }
+      lds_barrier();
+    }
+    __syncthreads();   // (the candidate states are visible to the producer)
+    return;
+  }
+
+  // ================================================================== producer
+  Env<NL> v;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) { v.q[d] = s.q[d * N + e]; v.qd[d] = s.qd[d * N + e]; }
+  uint32_t flags = s.flags[e];
+  const int s0 = c.replan ? steps0 : 0;
+  Traj<MP, NL, NB, false, false> tg;
+  tg.init(c, params + e * c.n_params, s.tables, s0, v.q, v.qd);
+  const double act_lo = __builtin_canonicalize(c.act_lo), act_hi = __builtin_canonicalize(c.act_hi);
+  const double pen = c.penalty;
+  double* pa = gr + Lay::oPA;
+  double* bl = gr + Lay::oBL;
+  double* ff = gr + Lay::oFF;
+  // resolution state: alive, segment length, terminated
+  bool alive = valid;
+  int L = 0;
+  bool term = false;
+  // numpy pairwise accumulators of committed full 8-blocks: level 1 (A) and the second half from
+  // s = 64, 72 (B; 80, 88, 96 in LDS).  Every committed sample's reward is acc_cost * -5e-8: the only
+  // other reward (a collision, env step 199) is the segment's last one, whose block is committed at
+  // the end (hr_simple_reward.py:33-47)
+  double A[8], B[kHpNR][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = 0.0;
+#pragma unroll
+    for (int q = 0; q < kHpNR; ++q) B[q][j] = 0.0;
+  }
+  auto plain = [&](int kk) __attribute__((always_inline)) { return pa[(kk % kHpPA) * 64 + lane] * -5e-8; };
+  // block b8 / 8 into the level-1 sums and the second halves that have started; x(j): reward of 8b + j
+  auto commit = [&](int b8, auto x) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double r = x(j);
+      if (b8 < 128) A[j] = (b8 == 0) ? r : A[j] + r;
+#pragma unroll
+      for (int q = 0; q < kHpNS; ++q) {
+        const int sq = kHpS0 + 8 * q;
+        if (sq > b8) continue;
+        if (q < kHpNR) {
+          B[q][j] = (sq == b8) ? r : B[q][j] + r;
+        } else {
+          double* bp = bl + ((q - kHpNR) * 8 + j) * 64 + lane;
+          *bp = (sq == b8) ? r : *bp + r;
+        }
+      }
+    }
+  };
+  for (int it = 0;; ++it) {
+    const int rp = (it + 1) & 1;
+    if (all_done(rp) || it > itmax) break;
+    // ---- resolve chunk cr = it - 2 (its consumers' stop codes were staged before the last barrier)
+    if (it >= 2) {
+      const int cr = it - 2;
+      if (alive) {
+        const uint8_t c0 = rs[((cr & 1) * 2) * 64 + lane], c1 = rs[((cr & 1) * 2 + 1) * 64 + lane];
+        if (c0 & 1) { L = 2 * cr + 1; term = (c0 & 2) != 0; alive = false; }
+        else if (c1 & 1) { L = 2 * cr + 2; term = (c1 & 2) != 0; alive = false; }
+        // samples 8b .. 8b + 7 all counted, none of them the last: commit block b
+        if (alive && (cr & 3) == 3) {
+          const int b8 = 2 * cr - 6;   // = 8 b
+          commit(b8, [&](int j) { return plain(b8 + j); });
+          const int sn = b8 + 8;   // block(0, sn) for a split start sn
+          if (sn >= kHpS0 && sn <= kHpS0 + 8 * (kHpNS - 1)) ff[((sn - kHpS0) / 8) * 64 + lane] = PairwiseSum::comb(A);
+        }
+      }
+    }
+    {
+      const uint64_t am = __ballot(alive);
+      if (lane == 0) al[it & 1] = am;
+    }
+    // ---- produce chunk it (samples 2 it, 2 it + 1) into buffer it & 1
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = 2 * it + i;
+      if (alive && k < Lst) {
+        float pos[NL], vel[NL];
+        tg.at(c, k, pos, vel);
+        // tracking controller + clip (black_box_wrapper.py:201-205; np.clip propagates NaN)
+        double a[NL];
+        float a32[NL];
+#pragma unroll
+        for (int d = 0; d < NL; ++d) {
+          if (CTRL == CTRL_PD) {
+            const double u = fadd(c.pg[d] * fsub((double)pos[d], v.q[d]), c.dg[d] * fsub((double)vel[d], v.qd[d]));
+            const double cl = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
+            a[d] = (u != u) ? u : cl;
+            a32[d] = 0.0f;
+          } else {
+            const float u = (CTRL == CTRL_VEL) ? vel[d] : pos[d];
+            a32[d] = np_clipf(u, c.act_lo32, c.act_hi32);
+            a[d] = (double)a32[d];
+          }
+        }
+        // np.sum(self._acc ** 2) (hr_simple_reward.py:48), acc = (a - q̇) / dt
+        // (base_reacher_direct.py:25): f32 once q̇ holds a float32 array (substep, fgx_kernels.h)
+        double acc_cost;
+        if (F32 && (flags & 1u)) {
+          float sq[NL];
+#pragma unroll
+          for (int d = 0; d < NL; ++d) {
+            const float ac = div_rcp(a32[d] - (float)v.qd[d], c.dt32, c.rcp_dt32);
+            sq[d] = ac * ac;
+          }
+          acc_cost = (double)np_sum<NL, float>([&](int d) { return sq[d]; }, [](float x, float y) { return x + y; });
+        } else {
+          double sq[NL];
+#pragma unroll
+          for (int d = 0; d < NL; ++d) {
+            const double ac = div_rcp64(a[d] - v.qd[d], c.dt, c.rcp_dt);
+            sq[d] = ac * ac;
+          }
+          acc_cost = np_sum<NL, double>([&](int d) { return sq[d]; }, [](double x, double y) { return x + y; });
+        }
+        pa[(k % kHpPA) * 64 + lane] = acc_cost;
+        double* rq = gr + Lay::oRQ + (size_t)((it & 1) * 2 + i) * NL * 64;
+        double* ra = gr + Lay::oRA + (size_t)((it & 1) * 2 + i) * NL * 64;
+        // q̇ = a; q += dt q̇ (base_reacher_direct.py:26-27)
+#pragma unroll
+        for (int d = 0; d < NL; ++d) {
+          v.qd[d] = a[d];
+          const double inc = F32 ? (double)(c.dt32 * a32[d]) : c.dt * v.qd[d];
+          v.q[d] = v.q[d] + inc;
+          rq[d * 64 + lane] = v.q[d];
+          ra[d * 64 + lane] = v.qd[d];
+        }
+        if (F32) flags |= 1u;
+      }
+    }
+    lds_barrier();
+  }
+  __syncthreads();   // the consumers' candidate states are visible
+  // the wave's inner steps: one atomic per wave (all lanes active here)
+  if (o.inner_steps) {
+    long long sum = valid ? L : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    count_inner(o.inner_steps, sum, lane == 0);
+  }
+  if (!valid) return;
+  const int own = (L - 1) & 1;   // the consumer that ran the last sample
+  const double* cd = cand + (int64_t)(own * CR) * N + e;
+  // the last sample's reward: np.dot([dist^2, acc, coll], [-1, -5e-8, -penalty]) at a collision or at
+  // env step 199, else acc * -5e-8 (hr_simple_reward.py:33-47)
+  const double acc_l = pa[((L - 1) % kHpPA) * 64 + lane];
+  const double rfin = (term || steps0 + L - 1 == 199)
+                          ? __builtin_fma(term ? 1.0 : 0.0, -pen, __builtin_fma(acc_l, -5e-8, cd[(int64_t)(2 * NL) * N] * -1.0))
+                          : acc_l * -5e-8;
+  auto reward_of = [&](int kk) __attribute__((always_inline)) { return kk == L - 1 ? rfin : plain(kk); };
+  // ---- the return: numpy pairwise sum of the L counted rewards (umath pairwise_sum: block(0, L) for
+  // L <= 128, else block(0, s) + block(s, L - s), s = (L / 2) & ~7; a block of >= 8 = its 8 slot sums
+  // combined, then the remainder added in order)
+  double ret;
+  if (L < 8) {
+    ret = 0.0;
+    for (int k = 0; k < L; ++k) ret = ret + reward_of(k);
+  } else {
+    if ((L & 7) == 0) commit(L - 8, [&](int j) { return reward_of(L - 8 + j); });   // the last block
+    double r8[8];
+    const int sfin = (L > 128) ? ((L / 2) & ~7) : 0;
+    const int qs = (sfin - kHpS0) / 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double x = A[j];
+#pragma unroll
+      for (int q = 0; q < kHpNS; ++q)
+        if (L > 128 && q == qs) x = (q < kHpNR) ? B[q][j] : bl[((q - kHpNR) * 8 + j) * 64 + lane];
+      r8[j] = x;
+    }
+    double u = PairwiseSum::comb(r8);
+    for (int k = L & ~7; k < L; ++k) u = u + reward_of(k);
+    ret = (L > 128) ? ff[qs * 64 + lane] + u : u;
+  }
+  // the BB-step outputs; k_hp_finish (below) completes the env: its final state, FK, the final
+  // observation and the VectorEnv auto-reset (episode_epilogue)
+  o.ret[e] = ret;
+  o.term[e] = term;
+  o.trunc[e] = steps0 + L >= c.max_steps;
+  o.tlen[e] = L;
+}
+
+// The episode epilogue of k_episode_hp's envs, one thread per env at full occupancy (in the pipeline
+// kernel its registers — PCG64 draws and rejection loops of the reset, FK, two observations — would
+// exceed the three-waves-per-SIMD budget): the final state is the candidate of the consumer that ran
+// the last sample; outputs, final observation, auto-reset and state write-back as k_episode's
+// (episode_epilogue, black_box_wrapper.py:241-253).
+template <int NL, bool F32>
+__global__ __launch_bounds__(256) void k_hp_finish(DevCfg c, DevState s, Outputs o) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= c.N) return;
+  const int64_t N = c.N;
+  constexpr int CR = hp_cand_rows<NL>();
+  const int L = o.tlen[e];
+  const double* cd = s.rew + (int64_t)(((L - 1) & 1) * CR) * N + e;
+  Env<NL> f;
+  load_env(c, s, e, f);
+#pragma unroll
+  for (int d = 0; d < NL; ++d) {
+    f.q[d] = cd[(int64_t)d * N];
+    f.qd[d] = cd[(int64_t)(NL + d) * N];
+  }
+  f.steps += L;
+  if (F32) f.flags |= 1u;
+  f.fk();
+  episode_epilogue(c, s, o, e, f, s.plans[e] + 1, L, o.ret[e], o.term[e] != 0, o.trunc[e] != 0, false);
+}
+
+inline size_t hp_lds_bytes(int nl, int groups) {
+  return (size_t)groups * (nl == 5 ? HpLayout<5>::GROUP : HpLayout<2>::GROUP) * sizeof(double);
+}
+static_assert(4 * HpLayout<5>::GROUP * sizeof(double) <= 160 * 1024, "k_episode_hp: four groups fit one CU's LDS");
+
+// k_episode_hp serves this step (FGX_HP=0 or FGX_EPISODE_KERNEL=classic|pair keep the others: A/B, tests)
+inline bool hp_applies(const DevCfg& c, const DevState& s, int mp, bool log, bool per_env_plans) {
+  if (const char* v = std::getenv("FGX_HP"))
+    if (std::strcmp(v, "0") == 0) return false;
+  if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))
+    if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "pair") == 0) return false;
+  return !log && c.env == ENV_HOLE && c.rew_fct == REW_SIMPLE && c.nl == 5 && c.nb == 5 &&
+         (mp == MP_PROMP || mp == MP_DMP || mp == MP_PRODMP) && !per_env_plans && !c.learn_tau && !c.learn_delay &&
+         !c.sched_state && !c.cond_desired && c.valid_flags == 0 && c.max_steps <= 200 && c.T <= 256 &&
+         s.rew != nullptr;
+}
+
+}  // namespace fgx
+
+// fgx_ep_hp.hip
+int fgx_launch_episode_hp(const fgx::DevCfg& c, const fgx::DevState& s, int mp, const float* params,
+                          const fgx::Outputs& o, hipStream_t stream, std::string& err);

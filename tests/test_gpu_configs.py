@@ -25,8 +25,8 @@ REPLAN25 = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(25)}}
 # (label, env id, override, envs per GPU, BB steps, expected kernel)
 CONFIGS = [
     ("config2", "fancy_ProMP/SimpleReacher-v0", None, 4096, 2, "k_episode_jl"),
-    ("config3", "fancy_ProDMP/HoleReacher-v0", None, 65536, 2, "k_episode"),
-    ("config3_shard", "fancy_ProDMP/HoleReacher-v0", None, 16384, 2, "k_episode_pair"),
+    ("config3", "fancy_ProDMP/HoleReacher-v0", None, 65536, 2, "k_episode_hp"),
+    ("config3_shard", "fancy_ProDMP/HoleReacher-v0", None, 16384, 2, "k_episode_hp"),
     ("config4_shard", "fancy_DMP/LongSimpleReacher-v0", None, 32768, 2, "k_episode_jl"),
     ("config5_shard", "fancy_ProDMP/SimpleReacher-v0", REPLAN25, 8192, 4, "k_episode_jl"),
     ("metric", "fancy_ProMP/LongSimpleReacher-v0", None, 65536, 2, "k_episode"),

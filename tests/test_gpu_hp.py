@@ -1,0 +1,127 @@
+"""k_episode_hp (fgx_hp.h: HoleReacher as a producer wave of dynamics feeding two consumer waves of
+FK / collision / reward through an LDS ring) against k_episode (FGX_EPISODE_KERNEL=classic): every
+output and the whole device state bit for bit over several BB steps, at batch sizes with partial
+workgroups, both workgroup shapes (one group of 64 envs per workgroup, four per workgroup), every MP
+kind and controller, replanning segments, the allow_* switches, NaN / inf parameters, and envs whose
+segments end by collision at every sample index (the return's pairwise split for every L)."""
+import numpy as np
+import pytest
+import torch
+
+import fancy_gym_crowd_amd as fgx
+from test_gpu_parity import DEV, np_
+
+pytestmark = pytest.mark.gpu
+
+REPLAN = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(50)}}
+CASES = [
+    # (env id, mp_config_override, env kwargs, N, BB steps, param scale)
+    ("fancy_ProDMP/HoleReacher-v0", None, {}, 1000, 3, 1.0),            # config 3's env (PD)
+    ("fancy_ProDMP/HoleReacher-v0", None, {}, 203, 3, 3.0),
+    ("fancy_ProMP/HoleReacher-v0", None, {}, 777, 3, 1.0),              # velocity controller (f32 actions)
+    ("fancy_DMP/HoleReacher-v0", None, {}, 512, 3, 0.3),
+    ("fancy_ProDMP/HoleReacher-v0", REPLAN, {}, 640, 6, 1.0),           # replanning segments
+    ("fancy_ProDMP/HoleReacher-v0", None, {"allow_self_collision": True}, 300, 3, 2.0),
+    ("fancy_ProMP/HoleReacher-v0", None, {"allow_wall_collision": True}, 257, 3, 1.0),
+    ("fancy_ProDMP/HoleReacher-v0", {"controller_kwargs": {"controller_type": "position"}}, {}, 129, 3, 1.0),
+]
+
+
+def _state(env):
+    return {k: np_(v) for k, v in env.get_state().items()}
+
+
+def _steps(env_id, over, kw, N, n_bb, plist, hp, monkeypatch, g=None, set_q=None):
+    """(every output and state array in order, the trajectory lengths of each BB step)"""
+    monkeypatch.delenv("FGX_HP", raising=False)
+    monkeypatch.delenv("FGX_EPISODE_KERNEL", raising=False)
+    monkeypatch.delenv("FGX_HP_G", raising=False)
+    if not hp:
+        monkeypatch.setenv("FGX_EPISODE_KERNEL", "classic")
+    if g is not None:
+        monkeypatch.setenv("FGX_HP_G", str(g))
+    env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=0, **kw)
+    assert env.episode_kernel() == ("k_episode_hp" if hp else "k_episode")
+    out = [np_(env.reset(seed=17)[0])]
+    if set_q is not None:
+        env.set_state(q=set_q)
+    tls = []
+    for b in range(n_bb):
+        obs, ret, te, tr, info = env.step(torch.from_numpy(plist[b]).to(DEV))
+        tls.append(np_(info["trajectory_length"]))
+        out += [np_(obs), np_(ret), np_(te), np_(tr), tls[-1], np_(info["final_observation"])]
+        out += list(_state(env).values())
+    return out, tls
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        np.testing.assert_array_equal(x, y, err_msg=f"output {i}")
+
+
+@pytest.mark.parametrize("g", [1, 4])
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_hp_equals_k_episode(ci, g, monkeypatch):
+    env_id, over, kw, N, n_bb, scale = CASES[ci]
+    probe = fgx.make(env_id, num_envs=8, device=DEV, mp_config_override=over, info_level=0, **kw)
+    rng = np.random.default_rng(100 + ci)
+    plist = [(rng.standard_normal((N, probe.n_params)) * scale).astype(np.float32) for _ in range(n_bb)]
+    del probe
+    a, _ = _steps(env_id, over, kw, N, n_bb, plist, True, monkeypatch, g=g)
+    b, _ = _steps(env_id, over, kw, N, n_bb, plist, False, monkeypatch)
+    _same(a, b)
+
+
+def test_hp_every_length_and_nonfinite(monkeypatch):
+    """Collisions at every sample index 1..200 (so every pairwise split of the return, L <= 128 and
+    every second-half start 64..96), NaN / inf parameters (NaN states never collide: full-length
+    segments) and huge joint angles (the joint-limit self-collision at the first sample)."""
+    env_id, N = "fancy_ProDMP/HoleReacher-v0", 4096
+    probe = fgx.make(env_id, num_envs=8, device=DEV, info_level=0)
+    P = probe.n_params
+    del probe
+    rng = np.random.default_rng(5)
+    plist = []
+    for b in range(4):
+        p = (rng.standard_normal((N, P)) * rng.uniform(0.2, 6.0, (N, 1))).astype(np.float32)
+        p[b::37] = np.nan
+        p[3 + b::41, 4] = np.inf
+        plist.append(p)
+    # joint angles past the limits on some envs: the self-collision test's joint-limit clause ends
+    # those segments at the first sample (base_reacher.py:38-39,111)
+    st = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
+    st.reset(seed=17)
+    q = np_(st.get_state()["q"]).copy()
+    del st
+    q[::53, 2] = 4.0
+    a, tla = _steps(env_id, None, {}, N, 4, plist, True, monkeypatch, g=4, set_q=q)
+    b, _ = _steps(env_id, None, {}, N, 4, plist, False, monkeypatch, set_q=q)
+    _same(a, b)
+    lengths = set(np.concatenate(tla).tolist())
+    assert 1 in lengths and 200 in lengths
+    assert len(lengths) > 150, len(lengths)   # collisions at most sample indices: every pairwise split
+
+
+def test_hp_full_batch_and_counter(monkeypatch):
+    """Config 3's size (65536 envs, four groups per workgroup): bit-identical to k_episode, and the
+    device inner-step counter (one atomic per consumer wave) equals the sum of trajectory lengths."""
+    env_id, N = "fancy_ProDMP/HoleReacher-v0", 65536
+    rng = np.random.default_rng(1234)
+    plist = [rng.standard_normal((N, 30), dtype=np.float32) for _ in range(2)]
+    a, _ = _steps(env_id, None, {}, N, 2, plist, True, monkeypatch)
+    b, _ = _steps(env_id, None, {}, N, 2, plist, False, monkeypatch)
+    _same(a, b)
+    monkeypatch.delenv("FGX_EPISODE_KERNEL", raising=False)
+    env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
+    assert env.episode_kernel() == "k_episode_hp"
+    env.reset(seed=0)
+    obs = torch.empty((N, env.out_dim), device=DEV)
+    ret = torch.empty(N, dtype=torch.float64, device=DEV)
+    te = torch.empty(N, dtype=torch.uint8, device=DEV)
+    tr = torch.empty(N, dtype=torch.uint8, device=DEV)
+    tl = torch.empty(N, dtype=torch.int32, device=DEV)
+    acc = env.new_inner_steps()
+    env.step_into(torch.from_numpy(plist[0]).to(DEV), obs, ret, te, tr, tl, inner_steps=acc)
+    torch.cuda.synchronize()
+    assert int(acc.sum().item()) == int(tl.to(torch.int64).sum().item())

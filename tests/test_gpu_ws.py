@@ -62,7 +62,7 @@ def test_episode_kernel_selection():
              ("fancy_DMP/LongSimpleReacher-v0", None, 32768, 0, "k_episode_jl"),     # config 4 shard
              ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_jl"),         # config 5 shard
              ("fancy_ProMP/SimpleReacher-v0", None, 65536, 0, "k_episode_jl"),       # 2 links: every size
-             ("fancy_ProDMP/HoleReacher-v0", None, 4096, 0, "k_episode_pair"),   # lane pairs
+             ("fancy_ProDMP/HoleReacher-v0", None, 4096, 0, "k_episode_hp"),     # producer / consumer pipeline
              ("fancy_ProDMP/HoleReacher-v0", None, 4096, 1, "k_episode_v2h"),     # per-step info, whole workgroups
              ("fancy_ProDMP/HoleReacher-v0", None, 4000, 1, "k_episode")]          # per-step info, a partial one
     for env_id, over, N, lvl, want in cases:

@@ -167,6 +167,20 @@ if __name__ == "__main__":
                 env_kwargs={"allow_wall_collision": True})
         episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_self_collision", reps=5,
                 env_kwargs={"allow_self_collision": True})
+    if "hp" in which:   # config 3: k_episode_hp (both workgroup shapes) against k_episode / k_episode_pair
+        import os
+        for n in (65536, 32768, 16384, 131072):
+            for label, env_set in (("hp", {}), ("hp G=1", {"FGX_HP_G": "1"}), ("hp G=4", {"FGX_HP_G": "4"}),
+                                   ("classic", {"FGX_EPISODE_KERNEL": "classic"}),
+                                   ("pair", {"FGX_EPISODE_KERNEL": "pair"})):
+                if label == "hp":
+                    continue
+                for k in ("FGX_HP_G", "FGX_EPISODE_KERNEL"):
+                    os.environ.pop(k, None)
+                os.environ.update(env_set)
+                episode("fancy_ProDMP/HoleReacher-v0", n, label=f"config3 {label}", reps=5)
+        for k in ("FGX_HP_G", "FGX_EPISODE_KERNEL"):
+            os.environ.pop(k, None)
     log_ids = [e for w, e in (("log", None), ("logsimple", "fancy_ProMP/LongSimpleReacher-v0"),
                               ("loghole", "fancy_ProDMP/HoleReacher-v0")) if w in which]
     if log_ids:   # info_level=2 (verbose 2 per-step arrays) through the public step(); logsimple /
