@@ -383,3 +383,22 @@ def test_validity_bound_semantics_follow_nep50():
     lo = np.float32(0.1)                                     # f32(0.1) > 0.1: the lower bound the same way
     assert val(np.array([lo, 0.0], np.float32), pos, pos)[0]
     assert not val(np.array([np.nextafter(lo, np.float32(0.0)), 0.0], np.float32), pos, pos)[0]
+
+
+def test_episode_kernel_lists_agree():
+    """fgx_episode_kernel's ids: include/fgx.h, INTEGRATION.md's entry-point table and the host's name
+    map (_lib.EPISODE_KERNELS) list the same kernels under the same numbers."""
+    import os
+    import re
+    from fancy_gym_crowd_amd import _lib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "fgx.h")).read()
+    doc = hdr[hdr.index("/* The kernel fgx_step launches"):hdr.index("int fgx_episode_kernel(")]
+    in_hdr = {int(k): v for k, v in re.findall(r"(\d+) = (k_episode\w*)", " ".join(doc.split()))}
+    integ = open(os.path.join(root, "INTEGRATION.md")).read()
+    row = [ln for ln in integ.splitlines() if ln.startswith("| `fgx_episode_kernel`")][0]
+    in_doc = {}
+    for k, v in re.findall(r"(\d+) (k_episode\w*|jp|ws|jl)", row):
+        in_doc[int(k)] = {"jp": "k_episode_jp", "ws": "k_episode_ws", "jl": "k_episode_jl"}.get(v, v)
+    assert in_hdr == _lib.EPISODE_KERNELS, (in_hdr, _lib.EPISODE_KERNELS)
+    assert in_doc == _lib.EPISODE_KERNELS, (in_doc, _lib.EPISODE_KERNELS)

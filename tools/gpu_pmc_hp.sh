@@ -12,6 +12,8 @@ for variant in ${VARIANTS:-hp classic}; do
     case $part in
       issue) grp="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" ;;
       mix)   grp="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT SQ_WAIT_ANY SQ_INSTS_VMEM_WR SQ_THREAD_CYCLES_VALU" ;;
+      icache) grp="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE" ;;
+      ifetch) grp="SQ_IFETCH SQ_INSTS SQ_INSTS_BRANCH SQ_INSTS_SMEM" ;;
       hbm)   grp="FETCH_SIZE" ;;
       wr)    grp="WRITE_SIZE" ;;
     esac
