@@ -4,6 +4,7 @@
 
 #include "fgx_kernels.h"
 #include "fgx_mfma.h"
+#include "fgx_traj_run.h"
 
 namespace fgx {
 
@@ -47,6 +48,9 @@ inline int launch_trajectory(const DevCfg& c, const DevState& s, const float* pa
   hipLaunchKernelGGL((k_traj_valu<MPV, NLV, NBV>), dim3(blocks), dim3(threads), 0, stream, c, s, params, dpos, dvel)
 #define X(NL)                                                                                 \
   if (c.nl == NL) {                                                                           \
+    const int rr = launch_traj_run<NL>(c, s, params, dpos, dvel, stream);                      \
+    if (rr == 0) return 0;                                                                    \
+    if (rr == 2) { err = hipGetErrorString(hipGetLastError()); return -2; }                   \
     const bool nb5 = c.nb == 5;                                                               \
     if (c.mp == MP_PROMP) { if (nb5) LAUNCH(MP_PROMP, NL, 5); else LAUNCH(MP_PROMP, NL, 0); } \
     else if (c.mp == MP_DMP) { if (nb5) LAUNCH(MP_DMP, NL, 5); else LAUNCH(MP_DMP, NL, 0); } \

@@ -4,7 +4,7 @@
 
 namespace fgx {
 
-template <int MP, int CTRL, int G>
+template <int MP, int CTRL, int G, bool INFO>
 static int launch_hp(const DevCfg& c, const DevState& s, const float* params, const Outputs& o, hipStream_t stream,
                      std::string& err) {
   if (c.stride != Traj<MP, 1, 5>::KS) {
@@ -12,13 +12,13 @@ static int launch_hp(const DevCfg& c, const DevState& s, const float* params, co
     return -1;
   }
   const size_t lds = hp_lds_bytes(5, G);
-  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_hp<MP, CTRL, 5, 5, G>,
+  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_hp<MP, CTRL, 5, 5, G, INFO>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
     err = "k_episode_hp: cannot raise the dynamic LDS limit";
     return -2;
   }
   const int64_t per = 64 * G;
-  hipLaunchKernelGGL((k_episode_hp<MP, CTRL, 5, 5, G>), dim3((unsigned)((c.N + per - 1) / per)), dim3(192 * G), lds,
+  hipLaunchKernelGGL((k_episode_hp<MP, CTRL, 5, 5, G, INFO>), dim3((unsigned)((c.N + per - 1) / per)), dim3(192 * G), lds,
                      stream, c, s, params, o);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { err = std::string("k_episode_hp launch: ") + hipGetErrorString(e); return -2; }
@@ -32,10 +32,15 @@ static int launch_hp(const DevCfg& c, const DevState& s, const float* params, co
 template <int MP, int G>
 static int launch_hp_ctrl(const DevCfg& c, const DevState& s, const float* params, const Outputs& o, hipStream_t stream,
                           std::string& err) {
+  // per-step arrays: the INFO instantiation
+  const bool info = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector;
   switch (c.ctrl) {
-    case CTRL_PD: return launch_hp<MP, CTRL_PD, G>(c, s, params, o, stream, err);
-    case CTRL_VEL: return launch_hp<MP, CTRL_VEL, G>(c, s, params, o, stream, err);
-    case CTRL_POS: return launch_hp<MP, CTRL_POS, G>(c, s, params, o, stream, err);
+    case CTRL_PD: return info ? launch_hp<MP, CTRL_PD, G, true>(c, s, params, o, stream, err)
+                              : launch_hp<MP, CTRL_PD, G, false>(c, s, params, o, stream, err);
+    case CTRL_VEL: return info ? launch_hp<MP, CTRL_VEL, G, true>(c, s, params, o, stream, err)
+                               : launch_hp<MP, CTRL_VEL, G, false>(c, s, params, o, stream, err);
+    case CTRL_POS: return info ? launch_hp<MP, CTRL_POS, G, true>(c, s, params, o, stream, err)
+                               : launch_hp<MP, CTRL_POS, G, false>(c, s, params, o, stream, err);
   }
   err = "bad ctrl_kind";
   return -1;

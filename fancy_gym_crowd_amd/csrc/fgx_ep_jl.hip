@@ -8,10 +8,10 @@
 #include <cstdlib>
 
 namespace {
-template <int MP, int NL, int NB>
+template <int MP, int NL, int NB, bool HLP = false>
 int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
               hipStream_t stream, std::string& err) {
-  using S = fgx::JlShape<NL>;
+  using S = fgx::JlShape<NL, HLP>;
   if constexpr (NB != 0) {
     if (c.stride != fgx::Traj<MP, 1, NB>::KS) {
       err = "basis table stride does not match the compiled layout";
@@ -22,16 +22,29 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
   if (const char* v = std::getenv("FGX_JL_GW")) gw = std::max(1, std::min(S::G, std::atoi(v)));   // experiments
   const int64_t per_block = (int64_t)S::WAVES * gw;
   const unsigned blocks = (unsigned)((c.N + per_block - 1) / per_block);
-  hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB>), dim3(blocks), dim3(S::THREADS), S::lds_bytes(), stream, c,
+  hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB, HLP>), dim3(blocks), dim3(S::THREADS), S::lds_bytes(), stream, c,
                      s, params, o, gw);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { err = std::string("k_episode_jl launch: ") + hipGetErrorString(e); return -2; }
   return 0;
 }
 
+// the helper form (fgx_jl.h, HLP): ProMP on the column table; FGX_JL_HELPER=1 / 0 forces it on / off
+inline bool jl_helper(const fgx::DevCfg& c) {
+  if (const char* v = std::getenv("FGX_JL_HELPER")) return v[0] == '1';
+  (void)c;
+  return false;
+}
+
 template <int MP, int NB>
 int launch_jl_nl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
                  hipStream_t stream, std::string& err) {
+  if constexpr (MP == fgx::MP_PROMP && NB == 5) {
+    if (jl_helper(c)) {
+      if (c.nl == 2) return launch_jl<MP, 2, NB, true>(c, s, params, o, stream, err);
+      if (c.nl == 5) return launch_jl<MP, 5, NB, true>(c, s, params, o, stream, err);
+    }
+  }
   if (c.nl == 2) return launch_jl<MP, 2, NB>(c, s, params, o, stream, err);
   if (c.nl == 5) return launch_jl<MP, 5, NB>(c, s, params, o, stream, err);
   err = "k_episode_jl: n_links not instantiated (supported: 2, 5)";

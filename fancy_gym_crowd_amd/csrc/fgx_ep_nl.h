@@ -10,6 +10,7 @@
 #include "fgx_dispatch.h"
 #include "fgx_learned.h"
 #include "fgx_step.h"
+#include "fgx_traj_run.h"
 
 #define FGX_NL_CAT2(a, b) a##b
 #define FGX_NL_CAT(a, b) FGX_NL_CAT2(a, b)
@@ -61,6 +62,9 @@ int nl_step_raw(const DevCfg& c, const DevState& s, const float* act, float* obs
 
 int nl_traj(const DevCfg& c, const DevState& s, const float* params, float* dpos, float* dvel, hipStream_t stream,
             std::string& err) {
+  const int rr = launch_traj_run<NLV>(c, s, params, dpos, dvel, stream);
+  if (rr == 0) return 0;
+  if (rr == 2) return hip_status("k_traj_run", err);
   const int threads = 256;
   const dim3 grid((unsigned)((c.N + threads - 1) / threads)), block(threads);
   if (c.mp == MP_PROMP) hipLaunchKernelGGL((k_traj_valu<MP_PROMP, NLV, 0>), grid, block, 0, stream, c, s, params, dpos, dvel);

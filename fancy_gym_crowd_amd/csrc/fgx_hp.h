@@ -33,14 +33,15 @@
 //
 // Served (hp_applies): HoleReacher with the simple reward function, 5 links, 5 basis functions per
 // joint, shared tables (no learned tau / delay), static replanning schedules, no
-// condition_on_desired, no validity checks, no per-step info, max_episode_steps <= 200.  Every output
-// and the whole env state equal k_episode's bit for bit (tests/test_gpu_hp.py).
+// condition_on_desired, no validity checks, max_episode_steps <= 200; with per-step info arrays
+// (info_level 1 / 2, a reward_aggregation reading step_rewards) the INFO instantiation.  Every output,
+// every per-step array and the whole env state equal k_episode's bit for bit (tests/test_gpu_hp.py).
 #pragma once
 #include <cstdlib>
 #include <cstring>
 #include <string>
 
-#include "fgx_kernels.h"
+#include "fgx_v2.h"
 
 namespace fgx {
 
@@ -71,7 +72,13 @@ struct HpLayout {
                        oFF = oBL + BL, oAL = oFF + FF;
 };
 
-template <int MP, int CTRL, int NL, int NB, int G>
+// INFO: the verbose-2 per-step arrays (black_box_wrapper.py:184-189,218-227,244-249) as well: the
+// producer writes the plan rows (positions / velocities) as it evaluates them, and at each chunk's
+// resolution the rows that need the counted / not-counted decision (step_actions from the action ring,
+// step_rewards, step_observations — cos / sin of q through obs_trig_fast, DESIGN.md §4.9 — NaN after
+// trajectory_length); the consumers write the env info rows of their samples (end_effector, is_collided,
+// is_success); the producer pads those after trajectory_length once every wave has left the loop.
+template <int MP, int CTRL, int NL, int NB, int G, bool INFO>
 __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, const float* __restrict__ params,
                                                        Outputs o) {
   using Lay = HpLayout<NL>;
@@ -137,6 +144,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
         jx[0] = 0.0; jy[0] = 0.0;
         bool lim = false, wc = false;
         double ang = 0.0, x = 0.0, y = 0.0;
+        double c0q = 0.0, s0q = 0.0;   // cos / sin of q[0] (the observation's)
 #pragma unroll
         for (int d = 0; d < NL; ++d) {
           const double qv = rq[d * 64 + lane];
@@ -144,6 +152,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
           ang = (d == 0) ? qv : ang + qv;
           double sn, cs;
           fgx_sincos(ang, &sn, &cs);
+          if (d == 0) { c0q = cs; s0q = sn; }
           x = (d == 0) ? cs : x + cs;
           y = (d == 0) ? sn : y + sn;
           jx[d + 1] = 0.0 + x;
@@ -165,6 +174,62 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
         }
         const bool coll = sc || wc;   // hr_simple_reward.py:19-53
         const bool stop = coll || k == Lst - 1;
+        if constexpr (INFO) {
+          // the per-step rows of this sample (black_box_wrapper.py:218-227; the producer rewrites the last
+          // sample's reward and pads every row past trajectory_length once the segment's end is known)
+          const uint32_t e4 = (uint32_t)e * 4u, e8 = (uint32_t)e * 8u;
+          const double* ra = gr + Lay::oRA + (size_t)((cpk & 1) * 2 + ci) * NL * 64;
+          if (o.step_actions)
+#pragma unroll
+            for (int d = 0; d < NL; ++d) st_row(o.step_actions, (int64_t)k * NL + d, N, e8, ra[d * 64 + lane]);
+          if (o.step_rewards)   // acc_cost * -5e-8 (hr_simple_reward.py:47)
+            st_row(o.step_rewards, (int64_t)k, N, e8, gr[Lay::oPA + (k % kHpPA) * 64 + lane] * -5e-8);
+          // the env info (hole_reacher.py:73-77, hr_simple_reward.py:33-53)
+          if (o.end_effector) {
+            st_row(o.end_effector, (int64_t)k * 2, N, e8, jx[NL]);
+            st_row(o.end_effector, (int64_t)k * 2 + 1, N, e8, jy[NL]);
+          }
+          if (o.is_collided) {
+            const bool sg = steps0 + k == 199 || coll;
+            const bool succ = sg && norm2(jx[NL] - gx, jy[NL] - gy) < 0.005 && !coll;
+            o.is_collided[(int64_t)k * N + e] = coll ? 1 : 0;
+            o.is_success[(int64_t)k * N + e] = succ ? 1 : 0;
+          }
+          if (o.step_obs) {
+            // emit_obs (hole_reacher.py:114-124, + TimeAwareObservation): cos q, sin q, q̇, hole width,
+            // end effector - goal, steps [, steps / max_steps].  cos / sin of q[0] are FK's first angle's;
+            // those of q[1..NL) through fgx_sincos_fast, each f32 checked against its error bound
+            // (obs_trig_fast's margin), else the exact fgx_sincos
+            const int X = c.full_dim;
+            const int64_t r0 = (int64_t)k * X;
+            st_row(o.step_obs, r0, N, e4, (float)c0q);
+            st_row(o.step_obs, r0 + NL, N, e4, (float)s0q);
+#pragma unroll
+            for (int d = 1; d < NL; ++d) {
+              const double qv = rq[d * 64 + lane];
+              double sn, cs;
+              fgx_sincos_fast(qv, &sn, &cs);
+              bool ok = __builtin_fabs(qv) < 0x1p20;
+              float fc = f32_checked(cs, 1e-15, ok), fs = f32_checked(sn, 1e-15, ok);
+              if (!ok) {
+                fgx_sincos(qv, &sn, &cs);
+                fc = (float)cs;
+                fs = (float)sn;
+              }
+              st_row(o.step_obs, r0 + d, N, e4, fc);
+              st_row(o.step_obs, r0 + NL + d, N, e4, fs);
+            }
+#pragma unroll
+            for (int d = 0; d < NL; ++d) st_row(o.step_obs, r0 + 2 * NL + d, N, e4, (float)ra[d * 64 + lane]);
+            st_row(o.step_obs, r0 + 3 * NL, N, e4, (float)hw);
+            st_row(o.step_obs, r0 + 3 * NL + 1, N, e4, (float)(jx[NL] - gx));
+            st_row(o.step_obs, r0 + 3 * NL + 2, N, e4, (float)(jy[NL] - gy));
+            const int stp = steps0 + k + 1;
+            st_row(o.step_obs, r0 + 3 * NL + 3, N, e4, (float)stp);
+            if (c.time_aware)
+              st_row(o.step_obs, r0 + 3 * NL + 4, N, e4, (float)((double)stp / (double)c.max_steps));
+          }
+        }
         rs[((cpk & 1) * 2 + ci) * 64 + lane] = (uint8_t)((stop ? 1 : 0) | (coll ? 2 : 0));
         if (stop) {
           // a candidate final state: this sample ends the segment unless an earlier one does; with the
@@ -195,9 +260,30 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
   const int s0 = c.replan ? steps0 : 0;
   Traj<MP, NL, NB, false, false> tg;
   tg.init(c, params + e * c.n_params, s.tables, s0, v.q, v.qd);
+  // every valid lane's plan starts on one row (always without replanning): the basis rows come through
+  // scalar loads (the constant address space), else per-lane loads of the same values
+  const int s0u = __builtin_amdgcn_readfirstlane(s0);
+  const bool s0_uni = __ballot(s0 != s0u) == 0;
+  tg.stab = (cfloat_ptr)(uintptr_t)s.tables + (size_t)s0u * tg.str();
   const double act_lo = __builtin_canonicalize(c.act_lo), act_hi = __builtin_canonicalize(c.act_hi);
   const double pen = c.penalty;
   double* pa = gr + Lay::oPA;
+  double pgx = 0.0, pgy = 0.0, phw = 0.0;   // (INFO: the observation's goal and hole width)
+  if constexpr (INFO) { pgx = s.goal[e]; pgy = s.goal[N + e]; phw = s.hole[N + e]; }
+  const uint32_t e4 = (uint32_t)e * 4u, e8 = (uint32_t)e * 8u;
+  const int X = c.full_dim;
+  const float fnan = __builtin_nanf("");
+  const double dnan = __builtin_nan("");
+  auto plan_rows = [&](int kk, const float* pos, const float* vel) __attribute__((always_inline)) {
+    if constexpr (INFO) {
+      if (o.positions)
+#pragma unroll
+        for (int d = 0; d < NL; ++d) {
+          st_row(o.positions, (int64_t)kk * NL + d, N, e4, pos[d]);
+          st_row(o.velocities, (int64_t)kk * NL + d, N, e4, vel[d]);
+        }
+    }
+  };
   double* bl = gr + Lay::oBL;
   double* ff = gr + Lay::oFF;
   // resolution state: alive, segment length, terminated
@@ -235,7 +321,10 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
       }
     }
   };
+  int it_end = 0;
+  int kp = 0;   // (INFO) the env's plan rows written so far
   for (int it = 0;; ++it) {
+    it_end = it;
     const int rp = (it + 1) & 1;
     if (all_done(rp) || it > itmax) break;
     // ---- resolve chunk cr = it - 2 (its consumers' stop codes were staged before the last barrier)
@@ -264,7 +353,10 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
       const int k = 2 * it + i;
       if (alive && k < Lst) {
         float pos[NL], vel[NL];
-        tg.at(c, k, pos, vel);
+        if (s0_uni) tg.template at<false, true>(c, k, pos, vel);   // rows by scalar loads: never queued
+        else tg.at(c, k, pos, vel);                                // behind the row stores (vmcnt)
+        plan_rows(k, pos, vel);
+        kp = k + 1;
         // tracking controller + clip (black_box_wrapper.py:201-205; np.clip propagates NaN)
         double a[NL];
         float a32[NL];
@@ -318,7 +410,20 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
     }
     lds_barrier();
   }
-  __syncthreads();   // the consumers' candidate states are visible
+  if constexpr (INFO) {
+    // the rest of every env's plan (black_box_wrapper.py:245-246: the full desired trajectory); the
+    // sample index stays wave-uniform (the row stores' base is), lanes join at their own kp
+    const int kmin = wave_min(valid ? kp : T);
+    for (int k = kmin; k < T; ++k) {
+      if (valid && k >= kp) {
+        float pos[NL], vel[NL];
+        if (s0_uni) tg.template at<false, true>(c, k, pos, vel);
+        else tg.at(c, k, pos, vel);
+        plan_rows(k, pos, vel);
+      }
+    }
+  }
+  __syncthreads();   // the consumers' candidate states and info rows are visible
   // the wave's inner steps: one atomic per wave (all lanes active here)
   if (o.inner_steps) {
     long long sum = valid ? L : 0;
@@ -326,6 +431,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
     count_inner(o.inner_steps, sum, lane == 0);
   }
+  const int Lmin = wave_min(valid ? L : T);   // (INFO padding: wave-uniform rows from here)
   if (!valid) return;
   const int own = (L - 1) & 1;   // the consumer that ran the last sample
   const double* cd = cand + (int64_t)(own * CR) * N + e;
@@ -359,6 +465,28 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
     double u = PairwiseSum::comb(r8);
     for (int k = L & ~7; k < L; ++k) u = u + reward_of(k);
     ret = (L > 128) ? ff[qs * 64 + lane] + u : u;
+  }
+  if constexpr (INFO) {
+    if (o.step_rewards) st_row(o.step_rewards, (int64_t)(L - 1), N, e8, rfin);
+    // the consumers' rows after trajectory_length (written by them for samples they ran past it, or
+    // never written): NaN, 0 for the flags (black_box_wrapper.py:244-249)
+    for (int k = Lmin; k < T; ++k) {
+      if (k < L) continue;   // (the row index stays wave-uniform for the row stores)
+      if (o.step_actions)
+#pragma unroll
+        for (int d = 0; d < NL; ++d) st_row(o.step_actions, (int64_t)k * NL + d, N, e8, dnan);
+      if (o.step_rewards) st_row(o.step_rewards, (int64_t)k, N, e8, dnan);
+      if (o.step_obs)
+        for (int p = 0; p < X; ++p) st_row(o.step_obs, (int64_t)k * X + p, N, e4, fnan);
+      if (o.end_effector) {
+        st_row(o.end_effector, (int64_t)k * 2, N, e8, dnan);
+        st_row(o.end_effector, (int64_t)k * 2 + 1, N, e8, dnan);
+      }
+      if (o.is_collided) {
+        o.is_collided[(int64_t)k * N + e] = 0;
+        o.is_success[(int64_t)k * N + e] = 0;
+      }
+    }
   }
   // the BB-step outputs; k_hp_finish (below) completes the env: its final state, FK, the final
   // observation and the VectorEnv auto-reset (episode_epilogue)
@@ -400,12 +528,16 @@ inline size_t hp_lds_bytes(int nl, int groups) {
 static_assert(4 * HpLayout<5>::GROUP * sizeof(double) <= 160 * 1024, "k_episode_hp: four groups fit one CU's LDS");
 
 // k_episode_hp serves this step (FGX_HP=0 or FGX_EPISODE_KERNEL=classic|pair keep the others: A/B, tests)
+// log: some per-step array is written (the INFO instantiation; FGX_V2=0 keeps the logging k_episode)
 inline bool hp_applies(const DevCfg& c, const DevState& s, int mp, bool log, bool per_env_plans) {
   if (const char* v = std::getenv("FGX_HP"))
     if (std::strcmp(v, "0") == 0) return false;
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))
     if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "pair") == 0) return false;
-  return !log && c.env == ENV_HOLE && c.rew_fct == REW_SIMPLE && c.nl == 5 && c.nb == 5 &&
+  if (log)
+    if (const char* v = std::getenv("FGX_V2"))
+      if (std::strcmp(v, "0") == 0) return false;
+  return c.env == ENV_HOLE && c.rew_fct == REW_SIMPLE && c.nl == 5 && c.nb == 5 &&
          (mp == MP_PROMP || mp == MP_DMP || mp == MP_PRODMP) && !per_env_plans && !c.learn_tau && !c.learn_delay &&
          !c.sched_state && !c.cond_desired && c.valid_flags == 0 && c.max_steps <= 200 && c.T <= 256 &&
          s.rew != nullptr;

@@ -33,13 +33,16 @@
 
 namespace fgx {
 
-template <int NL>
+typedef float jl_f4 __attribute__((ext_vector_type(4)));
+
+// HLP: one joint wave and one helper wave per workgroup (k_episode_jl's helper form, below)
+template <int NL, bool HLP = false>
 struct JlShape {
   static constexpr int G = 64 / NL;             // envs per wave
-  static constexpr int WAVES = 4;               // waves per workgroup
+  static constexpr int WAVES = HLP ? 1 : 4;     // joint waves per workgroup
   static constexpr int EPB = G * WAVES;         // envs per workgroup
   static constexpr int SPW = (8 + NL - 1) / NL; // pairwise slots owned per lane
-  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int THREADS = 64 * WAVES * (HLP ? 2 : 1);
   // gathered f64 per env: A, B, tail (8 each), cfk, q, qd, then cos / sin of the cumulative angles
   // (FK) and of every q (observation), then the env's stored steps, plan count, flags and goal
   static constexpr int GX = 25 + 6 * NL;
@@ -53,24 +56,44 @@ struct JlShape {
   // (90 -> 40, the LDS footprint shrinks; the 4 idle lanes do not write), 2 links stride 65
   // (32 -> 16, conflict-free; the gather area is larger anyway).  Writes stay conflict-free.
   static constexpr int XS = (G * NL < 64) ? G * NL + 1 : 65;
+  // HLP: after the exchange rows, the helper's two trajectory chunk buffers ([buf][4][lane] float4:
+  // P[0..3], P[4..7], V[0..3], V[4..7]) and its hand-over record (the pairwise slots, the look-ahead)
+  static constexpr size_t ex_bytes() { return ((size_t)WAVES * 16 * XS * sizeof(double) + 15) & ~(size_t)15; }
+  static constexpr size_t pv_bytes() { return HLP ? (size_t)2 * 4 * 64 * 16 : 0; }
+  static constexpr size_t ho_bytes() { return HLP ? (size_t)64 * (2 * SPW + 1) * sizeof(double) : 0; }
   static constexpr size_t lds_bytes() {
-    const size_t ex = (size_t)WAVES * 16 * XS * sizeof(double);
+    const size_t ex = ex_bytes() + pv_bytes() + ho_bytes();
     const size_t ga = (size_t)GF * EPB * sizeof(double);
     return ex > ga ? ex : ga;
   }
 };
 
-template <int MP, int NL, int NB>
 // gw: envs per wave actually used (<= G; experiments, FGX_JL_GW); LDS slots keep the compile-time
-// stride G
-__global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const float* __restrict__ params, Outputs o,
-                                                    int gw) {
-  using S = JlShape<NL>;
+// stride G.
+//
+// HLP (the helper form; ProMP with the column table only, host-selected): a workgroup is one joint
+// wave and one helper wave for the same G envs (lane l of both = env l / NL, joint l % NL).  The two
+// waves of a workgroup run on different SIMDs (profiles/r01_wave_placement.txt), and at the shard
+// sizes most SIMDs are otherwise idle.  Over the fast chunks the joint wave keeps only the f64
+// PD -> clip -> Euler chain (and the a^2 rows); the helper evaluates chunk ch + 1's trajectory into
+// an LDS buffer and reduces chunk ch - 1's a^2 rows into the pairwise slots while the joint wave runs
+// chunk ch, one workgroup barrier per chunk.  Both waves derive the fast-path decision from the same
+// loads (segment bounds, plan start, NaN-free guard), so they agree on the barrier count without
+// talking; after the last fast chunk the helper hands the pairwise slots and the look-ahead over and
+// the joint wave continues exactly as k_episode_jl (slow chunks, NaN re-run, gather, epilogue), the
+// helper wave's threads running the auto-resets of the split group.  Same operations in the same
+// order: bit-identical.
+template <int MP, int NL, int NB, bool HLP = false>
+__global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevCfg c, DevState s,
+                                                                         const float* __restrict__ params,
+                                                                         Outputs o, int gw) {
+  using S = JlShape<NL, HLP>;
   constexpr int G = S::G, EPB = S::EPB, SPW = S::SPW;
   constexpr int NBL = NB > 0 ? NB : 1;
   extern __shared__ double lds_jl[];
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const bool helper = HLP && (int)(threadIdx.x >> 6) >= S::WAVES;
+  const int w = helper ? (int)(threadIdx.x >> 6) - S::WAVES : (int)(threadIdx.x >> 6);
   constexpr int XS = S::XS;
   double* ex = lds_jl + w * (16 * XS);  // this wave's two chunk buffers: a^2 of sample j at [j * XS + lane]
   const int g = lane / NL, d = lane - g * NL;
@@ -80,7 +103,8 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   const bool valid = g < gw && e0 < N;
   const int64_t e = valid ? e0 : N - 1;   // clamped: loads stay in bounds, nothing is stored
   const uint64_t vmask = __ballot(valid);
-  const int64_t wst = ((int64_t)blockIdx.x * S::WAVES + w) * 64;   // diagnostics build: stamp slot of this wave
+  // diagnostics build: stamp slot of this wave (the helper's: none)
+  const int64_t wst = helper ? (int64_t)16384 * 64 : ((int64_t)blockIdx.x * S::WAVES + w) * 64;
   FGX_STAMP(o, wst, 6);
   FGX_STAMP(o, wst, 0);
 
@@ -395,9 +419,109 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
     if (kfk < 0x7fffffff) nf = min(nf, kfk / 8 + 1);
     return max(0, min(nf, nchunks));
   };
+  // ---- HLP: the two sides of the fast chunks
+  static_assert(!HLP || PKT, "the helper form runs ProMP's column-table chunks only");
+  jl_f4* pvb = (jl_f4*)((char*)lds_jl + S::ex_bytes());                    // [buf][4][lane]
+  double* hob = (double*)((char*)lds_jl + S::ex_bytes() + S::pv_bytes());  // [2 SPW + 1][lane]
+  auto hl_barrier = [] {   // both waves' LDS operations done, then the workgroup barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto pv_put = [&](int ch, const float* Pv, const float* Vv) __attribute__((always_inline)) {
+    jl_f4* b = pvb + (ch & 1) * 256 + lane;
+    b[0] = (jl_f4){Pv[0], Pv[1], Pv[2], Pv[3]};
+    b[64] = (jl_f4){Pv[4], Pv[5], Pv[6], Pv[7]};
+    b[128] = (jl_f4){Vv[0], Vv[1], Vv[2], Vv[3]};
+    b[192] = (jl_f4){Vv[4], Vv[5], Vv[6], Vv[7]};
+  };
+  auto pv_get = [&](int ch, float* Pv, float* Vv) __attribute__((always_inline)) {
+    const jl_f4* b = pvb + (ch & 1) * 256 + lane;
+    const jl_f4 p0 = b[0], p1 = b[64], v0 = b[128], v1 = b[192];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { Pv[j] = p0[j]; Pv[4 + j] = p1[j]; Vv[j] = v0[j]; Vv[4 + j] = v1[j]; }
+  };
+  // the helper: chunk 0's trajectory (Traj::at through the scalar rows, as run()), then per chunk ch
+  // the trajectory of chunk ch + 1 (with the plan-end patch of fast_iter) and the reduction of chunk
+  // ch - 1 in fast_range's phases; after the last chunk the hand-over record
+  auto helper_fast = [&](int nf, int na) __attribute__((always_inline)) {
+    traj(0, P, V, std::false_type{}, std::true_type{});
+    float vl = 0.0f;   // fast_iter's vlast: the last (patched) velocity of the previous chunk
+    auto patch = [&](int m, float* Vv) __attribute__((always_inline)) {
+      if (__builtin_expect(m == cpch, 0)) {
+        float prev = vl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float vj = Vv[j];
+          if (j == ip) Vv[j] = prev;
+          prev = vj;
+        }
+      }
+    };
+    patch(0, V);
+    vl = V[7];
+    pv_put(0, P, V);
+    hl_barrier();
+    for (int ch = 0; ch < nf; ++ch) {
+      const int k0 = ch * 8;
+      Cols cl;
+      traj_load(k0 + 8, cl);
+      double rv[SPW][NL];
+      if (ch >= 1) reduce_load(ch - 1, rv);
+      __builtin_amdgcn_sched_barrier(0);
+      traj_fast(k0 + 8, cl, Pn, Vn);
+      patch(ch + 1, Vn);
+      vl = Vn[7];
+      pv_put(ch + 1, Pn, Vn);
+      if (ch >= 1) {
+        if (ch < na) reduce_fast(rv, std::integral_constant<int, 1>{});
+        else reduce_fast(rv, std::integral_constant<int, 2>{});
+      }
+      if (ch == nf - 1) {
+#pragma unroll
+        for (int sl = 0; sl < SPW; ++sl) { hob[sl * 64 + lane] = A[sl]; hob[(SPW + sl) * 64 + lane] = B[sl]; }
+        hob[2 * SPW * 64 + lane] = __builtin_bit_cast(double, (f32x2){tg.cur[0], tg.vprev[0]});
+      }
+      hl_barrier();
+    }
+  };
+  // the joint wave: per chunk the f64 chain on the helper's trajectory; then chunk nf's trajectory
+  // (the slow chunks' first) and the hand-over
+  auto joint_fast = [&](int nf) __attribute__((always_inline)) {
+    hl_barrier();   // chunk 0's trajectory
+    for (int ch = 0; ch < nf; ++ch) {
+      pv_get(ch, P, V);
+      dyn(ch * 8, P, V, sq, std::true_type{}, std::integral_constant<int, 2>{});   // ProMP: NaN-free
+      write_sq(ch, sq);
+      plast = P[7];
+      vlast = V[7];
+      hl_barrier();
+    }
+    pv_get(nf, P, V);
+#pragma unroll
+    for (int sl = 0; sl < SPW; ++sl) { A[sl] = hob[sl * 64 + lane]; B[sl] = hob[(SPW + sl) * 64 + lane]; }
+    const f32x2 cv = __builtin_bit_cast(f32x2, hob[2 * SPW * 64 + lane]);
+    tg.cur[0] = cv[0];
+    tg.vprev[0] = cv[1];
+  };
+  // both waves decide the helper form's fast chunks from the same values
+  auto hlp_chunks = [&](int nchunks) __attribute__((always_inline)) -> int {
+    return (HLP && nchunks > 0 && s0_uni && Lmin == Lmax) ? fast_count(nchunks) : 0;
+  };
+
   auto run = [&](auto sc, auto exact) __attribute__((always_inline)) {
     const int nchunks = (Lmax + 7) / 8;
     if (nchunks == 0) return;
+    if constexpr (HLP && decltype(sc)::value && decltype(exact)::value == 0) {
+      const int nf = hlp_chunks(nchunks);
+      if (nf > 0) {
+        joint_fast(nf);
+        if (8 * nf == Lmin) { posl = plast; vell = vlast; }
+        FGX_STAMP(o, wst, 2);
+        slow_range(nf, nchunks, sc, exact);
+        return;
+      }
+    }
     traj(0, P, V, std::false_type{}, sc);
     int ch = 0;
     if constexpr (decltype(sc)::value && decltype(exact)::value == 0) {
@@ -430,16 +554,21 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   };
   nanm = 0;
   FGX_STAMP(o, wst, 1);
-  if (s0_uni) run(std::true_type{}, std::integral_constant<int, 0>{});
-  else run(std::false_type{}, std::integral_constant<int, 0>{});
-  if (__builtin_expect((nanm & vmask) != 0, 0)) {   // a NaN control: np.clip semantics from the start
-    wave_lds_sync();
-    restart();
-    if (s0_uni) run(std::true_type{}, std::integral_constant<int, 1>{});
-    else run(std::false_type{}, std::integral_constant<int, 1>{});
+  if (helper) {
+    const int nf = hlp_chunks((Lmax + 7) / 8);
+    if (nf > 0) helper_fast(nf, min(nf, __builtin_amdgcn_readlane(sg.hs, lead) / 8 + 1));
+  } else {
+    if (s0_uni) run(std::true_type{}, std::integral_constant<int, 0>{});
+    else run(std::false_type{}, std::integral_constant<int, 0>{});
+    if (__builtin_expect((nanm & vmask) != 0, 0)) {   // a NaN control: np.clip semantics from the start
+      wave_lds_sync();
+      restart();
+      if (s0_uni) run(std::true_type{}, std::integral_constant<int, 1>{});
+      else run(std::false_type{}, std::integral_constant<int, 1>{});
+    }
   }
 
-  if (valid && sg.stop && c.cond_desired) {   // black_box_wrapper.py:234-236
+  if (!helper && valid && sg.stop && c.cond_desired) {   // black_box_wrapper.py:234-236
     s.cond[d * N + e] = posl;
     s.cond[(NL + d) * N + e] = vell;
   }
@@ -452,7 +581,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   // whole waves), those threads run the resets concurrently with the first group's returns and
   // final observations.  Their inputs are loaded here, so that the loads land under the gather.
   constexpr int R0 = (EPB + 63) / 64 * 64;
-  constexpr bool SPLIT = R0 + EPB <= 64 * S::WAVES;
+  constexpr bool SPLIT = R0 + EPB <= S::THREADS;
   const int t1 = (int)threadIdx.x - R0, tw1 = t1 / G, tg1 = t1 - tw1 * G;
   const int64_t er = (int64_t)blockIdx.x * (S::WAVES * gw) + tw1 * gw + tg1;
   const bool rgrp = SPLIT && o.autoreset && t1 >= 0 && t1 < EPB && tg1 < gw && er < N;
@@ -466,14 +595,14 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   // the env's segment words and goal
   __syncthreads();   // 1: every wave is done with its chunk rows (the gather area overlaps them)
   double* ga = lds_jl;
-  if (g < G && d == 0) {
+  if (!helper && g < G && d == 0) {
     ga[(S::GX + 0) * EPB + slot] = (double)sg.steps;
     ga[(S::GX + 1) * EPB + slot] = (double)(sg.plans - 1);
     ga[(S::GX + 2) * EPB + slot] = (double)sg.flags;
     ga[(S::GX + 3) * EPB + slot] = gx;
     ga[(S::GX + 4) * EPB + slot] = gy;
   }
-  if (g < G) {
+  if (!helper && g < G) {
 #pragma unroll
     for (int sl = 0; sl < SPW; ++sl) {
       const int j = d + NL * sl;
@@ -490,7 +619,7 @@ __global__ __launch_bounds__(256) void k_episode_jl(DevCfg c, DevState s, const 
   __syncthreads();   // 2
   // the epilogue's trigonometry, one joint per lane: cos / sin of the cumulative angle q0 + ... + qd
   // (numpy cumsum order, Env::fk) and of qd itself (the observation, emit_obs)
-  if (g < G) {
+  if (!helper && g < G) {
     double ang = ga[25 * EPB + slot];
 #pragma unroll
     for (int k = 1; k < NL; ++k) {

@@ -125,3 +125,72 @@ def test_hp_full_batch_and_counter(monkeypatch):
     env.step_into(torch.from_numpy(plist[0]).to(DEV), obs, ret, te, tr, tl, inner_steps=acc)
     torch.cuda.synchronize()
     assert int(acc.sum().item()) == int(tl.to(torch.int64).sum().item())
+
+
+INFO_CASES = [
+    ("fancy_ProDMP/HoleReacher-v0", None, {}, 1000),
+    ("fancy_ProMP/HoleReacher-v0", None, {}, 203),                      # velocity controller
+    ("fancy_DMP/HoleReacher-v0", REPLAN, {}, 640),                      # replanning (TimeAwareObservation)
+    ("fancy_ProDMP/HoleReacher-v0", None, {"allow_self_collision": True}, 256),
+]
+
+
+@pytest.mark.parametrize("g", [1, 4])
+@pytest.mark.parametrize("info_level", [1, 2])
+@pytest.mark.parametrize("ci", range(len(INFO_CASES)))
+def test_hp_info_rows_equal_logging_kernel(ci, info_level, g, monkeypatch):
+    """k_episode_hp's INFO instantiation (verbose-2 per-step arrays: plan rows from the producer, the
+    other rows from the consumers, the last reward and the padding after trajectory_length from the
+    producer at the end) against the logging k_episode (FGX_V2=0): every per-step array, the outputs and
+    the device state bit for bit, NaN padding included, with NaN / inf parameters in some envs."""
+    env_id, over, kw, N = INFO_CASES[ci]
+    monkeypatch.setenv("FGX_HP_G", str(g))
+    a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
+    assert a.episode_kernel() == "k_episode_hp"
+    np.testing.assert_array_equal(np_(a.reset(seed=6)[0]), np_(b.reset(seed=6)[0]))
+    rng = np.random.default_rng(ci + 10 * info_level)
+    lengths = set()
+    for it in range(5):
+        p = (rng.standard_normal((N, a.n_params)) * 2).astype(np.float32)
+        p[it::29] = np.nan
+        p[1 + it::31, 3] = np.inf
+        p = torch.from_numpy(p).to(DEV)
+        monkeypatch.delenv("FGX_V2", raising=False)
+        ra = a.step(p)
+        monkeypatch.setenv("FGX_V2", "0")
+        rb = b.step(p)
+        monkeypatch.delenv("FGX_V2")
+        for x, y in zip(ra[:4], rb[:4]):
+            np.testing.assert_array_equal(np_(x), np_(y))
+        keys = [k for k in ra[4] if isinstance(ra[4][k], torch.Tensor) and not k.startswith("_")]
+        assert "is_collided" in keys and (info_level < 2 or "step_observations" in keys)
+        for k in keys:
+            np.testing.assert_array_equal(np_(ra[4][k]), np_(rb[4][k]), err_msg=k)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(np_(sa[k]), np_(sb[k]), err_msg=k)
+        lengths |= set(np_(ra[4]["trajectory_length"]).tolist())
+    assert len(lengths) > 5
+
+
+def test_hp_info_reward_aggregation(monkeypatch):
+    """reward_aggregation=np.max reads the device step_rewards of k_episode_hp's INFO instantiation
+    (info_level 0 requests only step_rewards): equal to the logging kernel's."""
+    over = {"black_box_kwargs": {"reward_aggregation": np.max}}
+    N = 512
+    a = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    b = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=N, device=DEV, mp_config_override=over, info_level=0)
+    assert a.episode_kernel() == "k_episode_hp"
+    a.reset(seed=3)
+    b.reset(seed=3)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        p = torch.from_numpy(rng.standard_normal((N, a.n_params), dtype=np.float32)).to(DEV)
+        monkeypatch.delenv("FGX_V2", raising=False)
+        ra = a.step(p)
+        monkeypatch.setenv("FGX_V2", "0")
+        rb = b.step(p)
+        monkeypatch.delenv("FGX_V2")
+        for x, y in zip(ra[:4], rb[:4]):
+            np.testing.assert_array_equal(np_(x), np_(y))

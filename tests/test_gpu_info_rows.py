@@ -44,9 +44,9 @@ def _rows(dev, ref, L, name, T):
 def test_info_rows_vs_oracle(ci, N):
     env_id, over = CASES[ci]
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
-    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher: k_episode_v2h at whole 256-env
-    # workgroups, else the logging k_episode
-    want = ("k_episode_v2h" if N % 256 == 0 else "k_episode") if "Hole" in env_id else "k_episode_v2"
+    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher (simple reward, 5 links): k_episode_hp
+    # (fgx_hp.h, its INFO instantiation)
+    want = "k_episode_hp" if "Hole" in env_id else "k_episode_v2"
     assert env.episode_kernel(info_level=2) == want
     spec = spec_of(env)
     tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
@@ -188,18 +188,29 @@ V2H_CASES = [
 ]
 
 
+def _hp_or_v2h(a, kern):
+    """the verbose-2 kernel under test: k_episode_hp where it applies (HoleReacher, simple reward, 5
+    links), else k_episode_v2h; kern == "v2h" runs with FGX_HP=0 (k_episode_v2h everywhere)"""
+    k = a.episode_kernel()
+    assert k == "k_episode_v2h" if kern == "v2h" else k in ("k_episode_v2h", "k_episode_hp"), k
+    return k
+
+
+@pytest.mark.parametrize("kern", ["default", "v2h"])
 @pytest.mark.parametrize("N", [512, 1024])
 @pytest.mark.parametrize("info_level", [1, 2])
 @pytest.mark.parametrize("ci", range(len(V2H_CASES)))
-def test_v2h_equals_logging_kernel(ci, info_level, N, monkeypatch):
+def test_v2h_equals_logging_kernel(ci, info_level, N, kern, monkeypatch):
     """k_episode_v2h (fgx_kernels.h: the logging body on waves 0..3, its per-step rows stored by waves
     4..7) against the logging k_episode (FGX_V2=0): every per-step array, the step outputs and the
     whole device state bit for bit over 6 BB steps with collisions (terminations at every sample),
     auto-resets and replanning segments."""
     env_id, over, kw = V2H_CASES[ci]
+    if kern == "v2h":
+        monkeypatch.setenv("FGX_HP", "0")
     a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
     b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
-    assert a.episode_kernel() == "k_episode_v2h"
+    _hp_or_v2h(a, kern)
     np.testing.assert_array_equal(np_(a.reset(seed=5)[0]), np_(b.reset(seed=5)[0]))
     rng = np.random.default_rng(ci + 10 * info_level)
     lengths = set()
@@ -224,19 +235,22 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, monkeypatch):
         assert len(lengths) > 2   # collisions ended episodes at different samples
 
 
+@pytest.mark.parametrize("kern", ["default", "v2h"])
 @pytest.mark.parametrize("env_id,over", [("fancy_ProDMP/HoleReacher-v0", None),
                                          ("fancy_ProMP/ViaPointReacher-v0",
                                           {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}})])
-def test_v2h_nonfinite_lanes(env_id, over, monkeypatch):
+def test_v2h_nonfinite_lanes(env_id, over, kern, monkeypatch):
     """k_episode_v2h with NaN / inf parameters and NaN / huge joint angles mixed into ordinary waves:
     a NaN action passes np.clip, NaN positions never collide, so those envs keep running with NaN
     state and their observation rows carry NaN cos / sin (the storing wave's placeholder, as sincos(NaN)
     in the logging kernel); bit for bit against the logging k_episode (FGX_V2=0).  Also a grid larger
     than one round of workgroups (N = 66048) and ViaPointReacher with a replanning schedule."""
+    if kern == "v2h":
+        monkeypatch.setenv("FGX_HP", "0")
     for N in (768, 66048):
         a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
         b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
-        assert a.episode_kernel() == "k_episode_v2h"
+        _hp_or_v2h(a, kern)
         a.reset(seed=9)
         b.reset(seed=9)
         rng = np.random.default_rng(N)
@@ -280,6 +294,7 @@ def test_v2h_given_plans_and_validity(mode, monkeypatch):
     logging k_episode."""
     N = 512
     env_id = "fancy_ProDMP/HoleReacher-v0"
+    monkeypatch.setenv("FGX_HP", "0")   # (k_episode_hp reports for the handle's own plans; v2h is tested here)
     kw = {}
     if mode == "validity":
         kw["traj_validity"] = fgx.TrajValidity(pos_low=[-1.2] * 5, pos_high=[1.2] * 5, invalid_return=-3.0,

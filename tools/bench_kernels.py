@@ -4,6 +4,7 @@ Prints one JSON line per measurement: config, envs, kernel time (HIP events on t
 stream), inner env-steps/s, algorithmic bytes and GB/s where meaningful.
 """
 import json
+import os
 import sys
 import time
 
@@ -63,9 +64,12 @@ def episode(env_id, N, over=None, label=None, reps=20, env_kwargs=None):
                           mean_traj_len=inner / N)), flush=True)
 
 
-def trajectory(env_id, N, force_valu=False):
-    over = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}} if force_valu else None
-    env = fgx.make(env_id, num_envs=N, device=dev, info_level=0, mp_config_override=over)
+def trajectory(env_id, N, force_valu=False, over=None, kernel=None):
+    """fgx_trajectory at N envs: k_traj_mfma, or (a replanning schedule that never fires before T, or
+    `over`) k_traj_run / k_traj_valu (FGX_TRAJ_VALU=1)"""
+    if over is None and force_valu:
+        over = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}
+    env = fgx.make(env_id, num_envs=N, device=dev, info_level=0, mp_config_override=over or None)
     env.reset(seed=0)
     params = torch.randn((N, env.n_params), device=dev)
     T, n = env.T, env.dof
@@ -78,9 +82,35 @@ def trajectory(env_id, N, force_valu=False):
     bytes_ = N * (env.n_params * 4 + 2 * T * n * 4)
     K = 8
     flops = N * n * T * 2 * 2 * K          # two K=8 GEMMs (pos + next/vel) incl. zero padding
-    print(json.dumps(dict(kernel="k_traj_valu" if force_valu else "k_traj_mfma", config=env_id, envs=N,
+    if kernel is None:
+        vk = bool(over) or env_id.startswith("fancy_DMP/")
+        kernel = ("k_traj_valu" if os.environ.get("FGX_TRAJ_VALU") else "k_traj_run") if vk else "k_traj_mfma"
+    print(json.dumps(dict(kernel=kernel, config=env_id, envs=N, over=str(over) if over else None,
+                          traj_ge=os.environ.get("FGX_TRAJ_GE"), traj_rc=os.environ.get("FGX_TRAJ_RC"),
                           kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
+
+
+def traj_run_scan():
+    """k_traj_run vs k_traj_valu on the plans k_traj_mfma does not take (65536 envs), then the
+    workgroup-shape A/B (FGX_TRAJ_GE / FGX_TRAJ_RC)"""
+    rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}
+    cases = [("fancy_DMP/LongSimpleReacher-v0", {}), ("fancy_DMP/HoleReacher-v0", {}),
+             ("fancy_ProMP/LongSimpleReacher-v0", rp), ("fancy_ProDMP/HoleReacher-v0", rp)]
+    for valu in (False, True):
+        if valu:
+            os.environ["FGX_TRAJ_VALU"] = "1"
+        for env_id, over in cases:
+            trajectory(env_id, 65536, over=over)
+        os.environ.pop("FGX_TRAJ_VALU", None)
+    shapes = {"dmp": [("17", "40"), ("25", "40"), ("32", "28"), ("51", "20"), ("51", "40")],
+              "run": [("4", "200"), ("16", "200"), ("8", "100"), ("16", "48"), ("32", "40")]}
+    for env_id, over in cases:
+        for ge, rc in shapes["dmp" if "DMP/" in env_id and "ProDMP" not in env_id else "run"]:
+            os.environ["FGX_TRAJ_GE"], os.environ["FGX_TRAJ_RC"] = ge, rc
+            trajectory(env_id, 65536, over=over)
+    os.environ.pop("FGX_TRAJ_GE", None)
+    os.environ.pop("FGX_TRAJ_RC", None)
 
 
 def mfma_ab(env_id="fancy_ProMP/LongSimpleReacher-v0", N=65536, reps=20):
@@ -181,6 +211,45 @@ if __name__ == "__main__":
                 episode("fancy_ProDMP/HoleReacher-v0", n, label=f"config3 {label}", reps=5)
         for k in ("FGX_HP_G", "FGX_EPISODE_KERNEL"):
             os.environ.pop(k, None)
+    if "jlh" in which:   # the 8-GPU shard sizes: k_episode_jl vs its helper form, alternated three times
+        for _ in range(3):
+            for n in (8192, 16384, 32768):
+                for h in ("0", "1"):
+                    os.environ["FGX_EPISODE_KERNEL"] = "jl"
+                    os.environ["FGX_JL_HELPER"] = h
+                    episode("fancy_ProMP/LongSimpleReacher-v0", n, label=f"metric jl helper={h}")
+        for k in ("FGX_EPISODE_KERNEL", "FGX_JL_HELPER"):
+            os.environ.pop(k, None)
+    if "hpinfo" in which:   # config 3's verbose-2 / info-level-1 public step(): k_episode_hp vs v2h vs logging
+        import os
+        for lvl in (2, 1):
+            for label, env_set in (("hp", {}), ("v2h", {"FGX_HP": "0"}), ("logging", {"FGX_V2": "0"})):
+                for k in ("FGX_HP", "FGX_V2"):
+                    os.environ.pop(k, None)
+                os.environ.update(env_set)
+                env = fgx.make("fancy_ProDMP/HoleReacher-v0", num_envs=65536, device=dev, info_level=lvl)
+                env.reset(seed=0)
+                params = torch.from_numpy(np.random.default_rng(1234).standard_normal((65536, env.n_params),
+                                                                                      dtype=np.float32)).to(dev)
+                for _ in range(2):
+                    info = env.step(params)[4]
+                torch.cuda.synchronize()
+                ib = sum(v.untyped_storage().nbytes() for kk, v in info.items() if isinstance(v, torch.Tensor)
+                         and v.dim() >= 2 and v.shape[1] == env.T)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    env.step(params)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / 5 * 1e3
+                print(json.dumps(dict(kernel=env.episode_kernel(), label=f"config3 step(info_level={lvl}) {label}",
+                                      envs=65536, us_per_step=us, info_bytes=ib,
+                                      info_GBps=ib / us / 1e3)), flush=True)
+                del env, info
+                torch.cuda.empty_cache()
+        for k in ("FGX_HP", "FGX_V2"):
+            os.environ.pop(k, None)
     log_ids = [e for w, e in (("log", None), ("logsimple", "fancy_ProMP/LongSimpleReacher-v0"),
                               ("loghole", "fancy_ProDMP/HoleReacher-v0")) if w in which]
     if log_ids:   # info_level=2 (verbose 2 per-step arrays) through the public step(); logsimple /
@@ -273,6 +342,8 @@ if __name__ == "__main__":
         for force in (False, True):
             trajectory("fancy_ProMP/LongSimpleReacher-v0", 65536, force)
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
+    if "trajrun" in which:
+        traj_run_scan()
     if "raw" in which:   # config 1 (step-based SimpleReacher) and the other step ids at 1M envs
         for env_id in ("fancy/SimpleReacher-v0", "fancy/LongSimpleReacher-v0", "fancy/HoleReacher-v0",
                        "fancy/ViaPointReacher-v0"):

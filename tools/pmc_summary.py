@@ -40,7 +40,7 @@ PARTS = ("fetch", "write", "issue", "busy", "mix", "mfma", "stall")
 
 def kernel_family(name):
     """'fgx::k_episode_jp<1, 5, 5>(...)' -> 'k_episode_jp' (the name env.episode_kernel() reports)."""
-    m = re.search(r"(k_episode(?:_jp|_ws|_jl|_w2|_pair|_v2h|_v2)?|k_traj_mfma|k_info_obs)\b", name)
+    m = re.search(r"(k_episode(?:_jp|_ws|_jl|_w2|_pair|_v2h|_v2|_hp)?|k_traj_mfma|k_info_obs)\b", name)
     return m.group(1) if m else None
 
 
