@@ -88,8 +88,8 @@ static bool episode_logs(const DevCfg& c, const Outputs& o) {
 static int launch_episode(const Handle& h, int mp, const float* params, const float* dpos, const float* dvel,
                           const Outputs& o, hipStream_t stream) {
   if (const NlOps* ops = nl_ops(h.dc.nl)) return ops->episode(h.dc, h.st, mp, params, dpos, dvel, o, stream, g_err);
-  // HoleReacher without per-step info: the producer / consumer pipeline (fgx_hp.h)
-  if (hp_applies(h.dc, h.st, mp, episode_logs(h.dc, o), h.st.plan_len != nullptr))
+  // HoleReacher up to info level 1: the producer / consumer pipeline (fgx_hp.h)
+  if (hp_applies(h.dc, h.st, mp, episode_logs(h.dc, o), o.positions || o.step_obs, h.st.plan_len != nullptr))
     return fgx_launch_episode_hp(h.dc, h.st, mp, params, o, stream, g_err);
   const bool gen = mp != MP_GIVEN && h.dc.nb != 5;   // generic basis-count instantiations
   if (h.dc.env == ENV_SIMPLE)
@@ -734,7 +734,7 @@ int fgx_episode_kernel(void* handle, int32_t info_level) {
   // the predicate launch_episode_nl uses: any per-step output, or the validity checks
   const bool log = info_level >= 1 || h->dc.valid_flags != 0;
   if (h->dc.nl == 2 || h->dc.nl == 5)
-    if (hp_applies(h->dc, h->st, mp, log, h->learned())) return EK_HP;
+    if (hp_applies(h->dc, h->st, mp, log, info_level >= 2, h->learned())) return EK_HP;
   return episode_kernel_choice(h->dc, mp, log, h->learned());
 }
 

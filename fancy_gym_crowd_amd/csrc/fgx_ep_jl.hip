@@ -8,7 +8,7 @@
 #include <cstdlib>
 
 namespace {
-template <int MP, int NL, int NB, bool HLP = false>
+template <int MP, int NL, int NB, int HLP = 0>
 int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
               hipStream_t stream, std::string& err) {
   using S = fgx::JlShape<NL, HLP>;
@@ -29,20 +29,24 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
   return 0;
 }
 
-// the helper form (fgx_jl.h, HLP): ProMP on the column table; FGX_JL_HELPER=1 / 0 forces it on / off
-inline bool jl_helper(const fgx::DevCfg& c) {
-  if (const char* v = std::getenv("FGX_JL_HELPER")) return v[0] == '1';
+// the helper form (fgx_jl.h, HLP 1 / 2): ProMP on the column table; FGX_JL_HELPER=0 / 1 / 2 forces
+inline int jl_helper(const fgx::DevCfg& c) {
+  if (const char* v = std::getenv("FGX_JL_HELPER")) return v[0] == '1' ? 1 : v[0] == '2' ? 2 : 0;
   (void)c;
-  return false;
+  return 0;
 }
 
 template <int MP, int NB>
 int launch_jl_nl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
                  hipStream_t stream, std::string& err) {
   if constexpr (MP == fgx::MP_PROMP && NB == 5) {
-    if (jl_helper(c)) {
-      if (c.nl == 2) return launch_jl<MP, 2, NB, true>(c, s, params, o, stream, err);
-      if (c.nl == 5) return launch_jl<MP, 5, NB, true>(c, s, params, o, stream, err);
+    const int h = jl_helper(c);
+    if (h == 1) {
+      if (c.nl == 2) return launch_jl<MP, 2, NB, 1>(c, s, params, o, stream, err);
+      if (c.nl == 5) return launch_jl<MP, 5, NB, 1>(c, s, params, o, stream, err);
+    } else if (h == 2) {
+      if (c.nl == 2) return launch_jl<MP, 2, NB, 2>(c, s, params, o, stream, err);
+      if (c.nl == 5) return launch_jl<MP, 5, NB, 2>(c, s, params, o, stream, err);
     }
   }
   if (c.nl == 2) return launch_jl<MP, 2, NB>(c, s, params, o, stream, err);

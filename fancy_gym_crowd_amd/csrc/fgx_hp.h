@@ -248,6 +248,9 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
       }
       lds_barrier();
     }
+    // the candidate states and this wave's rows complete before the producer reads the former and
+    // overwrites rows past trajectory_length (a workgroup barrier does not wait for stores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // (the candidate states are visible to the producer)
     return;
   }
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
     ret = (L > 128) ? ff[qs * 64 + lane] + u : u;
   }
   if constexpr (INFO) {
-    if (o.step_rewards) st_row(o.step_rewards, (int64_t)(L - 1), N, e8, rfin);
+    if (o.step_rewards) o.step_rewards[(int64_t)(L - 1) * N + e] = rfin;   // (per-lane row: no st_row)
     // the consumers' rows after trajectory_length (written by them for samples they ran past it, or
     // never written): NaN, 0 for the flags (black_box_wrapper.py:244-249)
     for (int k = Lmin; k < T; ++k) {
@@ -529,9 +532,16 @@ static_assert(4 * HpLayout<5>::GROUP * sizeof(double) <= 160 * 1024, "k_episode_
 
 // k_episode_hp serves this step (FGX_HP=0 or FGX_EPISODE_KERNEL=classic|pair keep the others: A/B, tests)
 // log: some per-step array is written (the INFO instantiation; FGX_V2=0 keeps the logging k_episode)
-inline bool hp_applies(const DevCfg& c, const DevState& s, int mp, bool log, bool per_env_plans) {
-  if (const char* v = std::getenv("FGX_HP"))
+// heavy: the verbose-2 rows (planned positions / velocities, step observations): k_episode_v2h stays
+// faster there (65536 envs: 1026 vs 1637 us, profiles/r05_s9_jlhelper_traj_hpinfo.jsonl), so k_episode_hp takes
+// them only when forced (FGX_HP=1); FGX_HP=0 never takes it
+inline bool hp_applies(const DevCfg& c, const DevState& s, int mp, bool log, bool heavy, bool per_env_plans) {
+  bool force = false;
+  if (const char* v = std::getenv("FGX_HP")) {
     if (std::strcmp(v, "0") == 0) return false;
+    force = std::strcmp(v, "1") == 0;
+  }
+  if (heavy && !force) return false;
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))
     if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "pair") == 0) return false;
   if (log)

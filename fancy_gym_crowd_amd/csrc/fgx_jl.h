@@ -35,8 +35,10 @@ namespace fgx {
 
 typedef float jl_f4 __attribute__((ext_vector_type(4)));
 
-// HLP: one joint wave and one helper wave per workgroup (k_episode_jl's helper form, below)
-template <int NL, bool HLP = false>
+// HLP: one joint wave and one helper wave per workgroup (k_episode_jl's helper form, below);
+// 1: the helper hands over f32 trajectory chunks and the joint wave writes a^2, 2: f64 chunks (the
+// conversions on the helper) and the joint wave writes a (the squares on the helper)
+template <int NL, int HLP = 0>
 struct JlShape {
   static constexpr int G = 64 / NL;             // envs per wave
   static constexpr int WAVES = HLP ? 1 : 4;     // joint waves per workgroup
@@ -56,10 +58,12 @@ struct JlShape {
   // (90 -> 40, the LDS footprint shrinks; the 4 idle lanes do not write), 2 links stride 65
   // (32 -> 16, conflict-free; the gather area is larger anyway).  Writes stay conflict-free.
   static constexpr int XS = (G * NL < 64) ? G * NL + 1 : 65;
-  // HLP: after the exchange rows, the helper's two trajectory chunk buffers ([buf][4][lane] float4:
-  // P[0..3], P[4..7], V[0..3], V[4..7]) and its hand-over record (the pairwise slots, the look-ahead)
+  // HLP: after the exchange rows, the helper's two trajectory chunk buffers ([buf][PVQ][lane] 16-B
+  // quads: HLP 1 P[0..3], P[4..7], V[0..3], V[4..7] as f32; HLP 2 P[0..1] .. V[6..7] as f64) and its
+  // hand-over record (the pairwise slots, the look-ahead)
+  static constexpr int PVQ = HLP == 2 ? 8 : 4;
   static constexpr size_t ex_bytes() { return ((size_t)WAVES * 16 * XS * sizeof(double) + 15) & ~(size_t)15; }
-  static constexpr size_t pv_bytes() { return HLP ? (size_t)2 * 4 * 64 * 16 : 0; }
+  static constexpr size_t pv_bytes() { return HLP ? (size_t)2 * PVQ * 64 * 16 : 0; }
   static constexpr size_t ho_bytes() { return HLP ? (size_t)64 * (2 * SPW + 1) * sizeof(double) : 0; }
   static constexpr size_t lds_bytes() {
     const size_t ex = ex_bytes() + pv_bytes() + ho_bytes();
@@ -83,7 +87,7 @@ struct JlShape {
 // the joint wave continues exactly as k_episode_jl (slow chunks, NaN re-run, gather, epilogue), the
 // helper wave's threads running the auto-resets of the split group.  Same operations in the same
 // order: bit-identical.
-template <int MP, int NL, int NB, bool HLP = false>
+template <int MP, int NL, int NB, int HLP = 0>
 __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevCfg c, DevState s,
                                                                          const float* __restrict__ params,
                                                                          Outputs o, int gw) {
@@ -428,18 +432,47 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
+  typedef double jl_d2 __attribute__((ext_vector_type(2)));
   auto pv_put = [&](int ch, const float* Pv, const float* Vv) __attribute__((always_inline)) {
-    jl_f4* b = pvb + (ch & 1) * 256 + lane;
-    b[0] = (jl_f4){Pv[0], Pv[1], Pv[2], Pv[3]};
-    b[64] = (jl_f4){Pv[4], Pv[5], Pv[6], Pv[7]};
-    b[128] = (jl_f4){Vv[0], Vv[1], Vv[2], Vv[3]};
-    b[192] = (jl_f4){Vv[4], Vv[5], Vv[6], Vv[7]};
+    jl_f4* b = pvb + (ch & 1) * (S::PVQ * 64) + lane;
+    if constexpr (HLP == 2) {
+      jl_d2* bd = (jl_d2*)b;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bd[i * 64] = (jl_d2){(double)Pv[2 * i], (double)Pv[2 * i + 1]};
+        bd[(4 + i) * 64] = (jl_d2){(double)Vv[2 * i], (double)Vv[2 * i + 1]};
+      }
+    } else {
+      b[0] = (jl_f4){Pv[0], Pv[1], Pv[2], Pv[3]};
+      b[64] = (jl_f4){Pv[4], Pv[5], Pv[6], Pv[7]};
+      b[128] = (jl_f4){Vv[0], Vv[1], Vv[2], Vv[3]};
+      b[192] = (jl_f4){Vv[4], Vv[5], Vv[6], Vv[7]};
+    }
   };
   auto pv_get = [&](int ch, float* Pv, float* Vv) __attribute__((always_inline)) {
-    const jl_f4* b = pvb + (ch & 1) * 256 + lane;
-    const jl_f4 p0 = b[0], p1 = b[64], v0 = b[128], v1 = b[192];
+    const jl_f4* b = pvb + (ch & 1) * (S::PVQ * 64) + lane;
+    if constexpr (HLP == 2) {
+      const jl_d2* bd = (const jl_d2*)b;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { Pv[j] = p0[j]; Pv[4 + j] = p1[j]; Vv[j] = v0[j]; Vv[4 + j] = v1[j]; }
+      for (int i = 0; i < 4; ++i) {
+        const jl_d2 p = bd[i * 64], v = bd[(4 + i) * 64];
+        Pv[2 * i] = (float)p[0]; Pv[2 * i + 1] = (float)p[1];
+        Vv[2 * i] = (float)v[0]; Vv[2 * i + 1] = (float)v[1];
+      }
+    } else {
+      const jl_f4 p0 = b[0], p1 = b[64], v0 = b[128], v1 = b[192];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { Pv[j] = p0[j]; Pv[4 + j] = p1[j]; Vv[j] = v0[j]; Vv[4 + j] = v1[j]; }
+    }
+  };
+  auto pv_get_d = [&](int ch, double* Pd, double* Vd) __attribute__((always_inline)) {   // HLP 2
+    const jl_d2* bd = (const jl_d2*)(pvb + (ch & 1) * (S::PVQ * 64) + lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const jl_d2 p = bd[i * 64], v = bd[(4 + i) * 64];
+      Pd[2 * i] = p[0]; Pd[2 * i + 1] = p[1];
+      Vd[2 * i] = v[0]; Vd[2 * i + 1] = v[1];
+    }
   };
   // the helper: chunk 0's trajectory (Traj::at through the scalar rows, as run()), then per chunk ch
   // the trajectory of chunk ch + 1 (with the plan-end patch of fast_iter) and the reduction of chunk
@@ -471,6 +504,12 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
       __builtin_amdgcn_sched_barrier(0);
       traj_fast(k0 + 8, cl, Pn, Vn);
       patch(ch + 1, Vn);
+      if constexpr (HLP == 2) {   // the joint wave wrote a: the squares here
+#pragma unroll
+        for (int sl = 0; sl < SPW; ++sl)
+#pragma unroll
+          for (int dd = 0; dd < NL; ++dd) rv[sl][dd] = rv[sl][dd] * rv[sl][dd];
+      }
       vl = Vn[7];
       pv_put(ch + 1, Pn, Vn);
       if (ch >= 1) {
@@ -490,11 +529,32 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   auto joint_fast = [&](int nf) __attribute__((always_inline)) {
     hl_barrier();   // chunk 0's trajectory
     for (int ch = 0; ch < nf; ++ch) {
-      pv_get(ch, P, V);
-      dyn(ch * 8, P, V, sq, std::true_type{}, std::integral_constant<int, 2>{});   // ProMP: NaN-free
+      if constexpr (HLP == 2) {
+        // dyn's fast, NaN-free form on the helper's f64 chunk, writing a (the last fast chunk a^2:
+        // the slow chunks reduce it here)
+        double Pd[8], Vd[8];
+        pv_get_d(ch, Pd, Vd);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const double u = fadd(pg * fsub(Pd[j], q), dg * fsub(Vd[j], qd));
+          const double a = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
+          qd = fadd(qd, dt * a);
+          q = fadd(q, dt * qd);
+          sq[j] = a;
+        }
+        if (ch == nf - 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sq[j] = sq[j] * sq[j];
+        }
+        plast = (float)Pd[7];
+        vlast = (float)Vd[7];
+      } else {
+        pv_get(ch, P, V);
+        dyn(ch * 8, P, V, sq, std::true_type{}, std::integral_constant<int, 2>{});   // ProMP: NaN-free
+        plast = P[7];
+        vlast = V[7];
+      }
       write_sq(ch, sq);
-      plast = P[7];
-      vlast = V[7];
       hl_barrier();
     }
     pv_get(nf, P, V);

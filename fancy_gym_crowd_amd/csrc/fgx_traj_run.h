@@ -47,7 +47,7 @@ inline int traj_run_cus() {
 template <int MP, int NL, int NB, bool V4>
 __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState s, const float* __restrict__ params,
                                                               float* __restrict__ dpos, float* __restrict__ dvel,
-                                                              int GE, int RC) {
+                                                              int GE, int RC, int nt) {
   constexpr bool SEQ = MP == MP_DMP;                   // per-joint lanes through every chunk
   using TrajT = Traj<MP, SEQ ? 1 : NL, NB>;
   extern __shared__ float4 lds_run[];
@@ -84,8 +84,14 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
       gchar* base = uniform_ptr(out + ((e0 + j) * T + row0) * NL);
       const float* src = reg + j * ESR;
       if constexpr (V4) {
-        for (int ch = lane; ch < nf / 4; ch += 64)
-          *(__attribute__((address_space(1))) f32x4*)(base + 16u * (uint32_t)ch) = *reinterpret_cast<const f32x4*>(src + 4 * ch);
+        if (nt) {   // (A/B: streaming stores)
+          for (int ch = lane; ch < nf / 4; ch += 64)
+            __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(src + 4 * ch),
+                                        (__attribute__((address_space(1))) f32x4*)(base + 16u * (uint32_t)ch));
+        } else {
+          for (int ch = lane; ch < nf / 4; ch += 64)
+            *(__attribute__((address_space(1))) f32x4*)(base + 16u * (uint32_t)ch) = *reinterpret_cast<const f32x4*>(src + 4 * ch);
+        }
       } else {
         for (int f = lane; f < nf; f += 64) *(__attribute__((address_space(1))) float*)(base + 4u * (uint32_t)f) = src[f];
       }
@@ -170,10 +176,17 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   }
 }
 
-// workgroup shape of k_traj_run: GE envs per group, RC rows per chunk (RC >= T: whole runs).
-// FGX_TRAJ_GE / FGX_TRAJ_RC override (A/B).
+// workgroup shape of k_traj_run: GE envs per group, RC rows per chunk (RC >= T: whole runs), nt:
+// streaming stores.  Chosen from the A/B at 65536 envs, T = 200, 5 links
+// (profiles/r05_s10_traj_hpinfo.jsonl, us per launch):
+//   * ProMP (replanning): whole runs of 8 envs (two workgroups per CU) 102 us, 5.2 TB/s;
+//   * ProDMP (replanning, a 402-row table in LDS): 16 envs x 64 rows with streaming stores 151 us
+//     (whole runs of 8 envs 303-313 us: the table leaves room for one workgroup per CU);
+//   * DMP: one wave of joint lanes (64 / dof envs) x 40 rows 167 us (12 x 32 / 64: 174 / 193;
+//     17 / 25 envs: 175-185; streaming stores no better).
+// FGX_TRAJ_GE / FGX_TRAJ_RC / FGX_TRAJ_NT=0|1 override (A/B).
 struct TrajRunShape {
-  int GE, RC;
+  int GE, RC, nt;
   size_t lds;
 };
 inline size_t traj_run_lds(const DevCfg& c, int GE, int RC) {
@@ -182,13 +195,16 @@ inline size_t traj_run_lds(const DevCfg& c, int GE, int RC) {
 inline TrajRunShape traj_run_shape(const DevCfg& c) {
   const int nl = c.nl, T = c.T;
   const size_t budget = 80 * 1024;   // two workgroups per CU
-  int GE, RC;
+  int GE, RC, nt = 0;
   // RC * nl a multiple of 4 (whole 16-B chunks per piece)
   auto rc_align = [&](int rc) { while (rc > 4 && (rc * nl) % 4) --rc; return rc; };
   if (c.mp == MP_DMP) {
-    GE = kTrajRunThreads / nl;
-    const size_t per = budget > traj_run_lds(c, GE, 0) ? (budget - traj_run_lds(c, GE, 0)) / (2 * (size_t)GE * 4) : 0;
-    RC = rc_align(std::max(4, (int)std::min<size_t>((size_t)T, per / nl)));
+    GE = 64 / nl;
+    RC = rc_align(std::min(T, 40));
+  } else if (c.mp == MP_PRODMP) {
+    GE = 16;
+    RC = rc_align(std::min(T, 64));
+    nt = 1;
   } else {
     GE = 32;
     while (GE > 1 && traj_run_lds(c, GE, T) > budget) GE >>= 1;
@@ -201,8 +217,9 @@ inline TrajRunShape traj_run_shape(const DevCfg& c) {
   if (const char* v = std::getenv("FGX_TRAJ_GE")) GE = std::max(1, std::min(kTrajRunThreads, std::atoi(v)));
   if (c.mp == MP_DMP) GE = std::min(GE, kTrajRunThreads / nl);
   if (const char* v = std::getenv("FGX_TRAJ_RC")) RC = std::max(1, std::min(T, std::atoi(v)));
+  if (const char* v = std::getenv("FGX_TRAJ_NT")) nt = v[0] == '1';
   RC = std::min(RC, T);
-  return {GE, RC, traj_run_lds(c, GE, RC)};
+  return {GE, RC, nt, traj_run_lds(c, GE, RC)};
 }
 
 // 0: launched; 1: not applicable (the caller runs k_traj_valu); 2: launch error
@@ -215,13 +232,14 @@ inline int launch_traj_run(const DevCfg& c, const DevState& s, const float* para
   if (sh.lds > 160 * 1024) return 1;
   const bool v4 = ((c.T * NL) % 4) == 0 && ((sh.RC * NL) % 4) == 0 && (((uintptr_t)dpos | (uintptr_t)dvel) & 15) == 0;
   const int64_t groups = (c.N + sh.GE - 1) / sh.GE;
+  const int nt = sh.nt;
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(sh.lds, 1)));
   const int blocks = (int)std::min<int64_t>(groups, (int64_t)traj_run_cus() * per_cu);
   const dim3 grid(blocks), block(kTrajRunThreads);
 #define RUN(MPV, NBV, V4V)                                                                                      \
   launch_lds((const void*)k_traj_run<MPV, NL, NBV, V4V>, sh.lds, [&] {                                        \
     hipLaunchKernelGGL((k_traj_run<MPV, NL, NBV, V4V>), grid, block, sh.lds, stream, c, s, params, dpos, dvel, \
-                       sh.GE, sh.RC);                                                                         \
+                       sh.GE, sh.RC, nt);                                                                     \
   })
 #define BY_V4(MPV, NBV) \
   if (v4) RUN(MPV, NBV, true); else RUN(MPV, NBV, false)

@@ -145,6 +145,8 @@ def test_hp_info_rows_equal_logging_kernel(ci, info_level, g, monkeypatch):
     the device state bit for bit, NaN padding included, with NaN / inf parameters in some envs."""
     env_id, over, kw, N = INFO_CASES[ci]
     monkeypatch.setenv("FGX_HP_G", str(g))
+    if info_level >= 2:
+        monkeypatch.setenv("FGX_HP", "1")   # (the verbose-2 rows: k_episode_v2h by default)
     a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
     b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
     assert a.episode_kernel() == "k_episode_hp"

@@ -41,12 +41,17 @@ def _rows(dev, ref, L, name, T):
 
 @pytest.mark.parametrize("N", [256, 1000, 203])
 @pytest.mark.parametrize("ci", range(len(CASES)))
-def test_info_rows_vs_oracle(ci, N):
+def test_info_rows_vs_oracle(ci, N, monkeypatch):
     env_id, over = CASES[ci]
+    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher (simple reward, 5 links): k_episode_v2h,
+    # and (N = 1000, FGX_HP=1) k_episode_hp's INFO instantiation (fgx_hp.h)
+    hp = "Hole" in env_id and N == 1000
+    if hp:
+        monkeypatch.setenv("FGX_HP", "1")
     env = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=2)
-    # SimpleReacher + PD: k_episode_v2 (fgx_v2.h); HoleReacher (simple reward, 5 links): k_episode_hp
-    # (fgx_hp.h, its INFO instantiation)
-    want = "k_episode_hp" if "Hole" in env_id else "k_episode_v2"
+    # (k_episode_v2h at a multiple of 256 envs, else the logging k_episode)
+    hole = "k_episode_hp" if hp else ("k_episode_v2h" if N % 256 == 0 else "k_episode")
+    want = hole if "Hole" in env_id else "k_episode_v2"
     assert env.episode_kernel(info_level=2) == want
     spec = spec_of(env)
     tabs = oracle_tables_dict(spec, env)   # the oracle's own tables (== the device's, bit for bit)
@@ -188,15 +193,19 @@ V2H_CASES = [
 ]
 
 
-def _hp_or_v2h(a, kern):
-    """the verbose-2 kernel under test: k_episode_hp where it applies (HoleReacher, simple reward, 5
-    links), else k_episode_v2h; kern == "v2h" runs with FGX_HP=0 (k_episode_v2h everywhere)"""
-    k = a.episode_kernel()
-    assert k == "k_episode_v2h" if kern == "v2h" else k in ("k_episode_v2h", "k_episode_hp"), k
+def _hp_or_v2h(a, kern, info_level=2):
+    """the kernel under test: k_episode_hp where it applies (HoleReacher, simple reward, 5 links: info
+    level 1 by default, level 2 with kern == "hp", FGX_HP=1), else k_episode_v2h; kern == "v2h" runs
+    with FGX_HP=0 (k_episode_v2h everywhere)"""
+    k = a.episode_kernel(info_level=info_level)
+    if kern == "v2h" or (kern == "default" and info_level >= 2):
+        assert k == "k_episode_v2h", k
+    else:
+        assert k in ("k_episode_v2h", "k_episode_hp"), k
     return k
 
 
-@pytest.mark.parametrize("kern", ["default", "v2h"])
+@pytest.mark.parametrize("kern", ["default", "v2h", "hp"])
 @pytest.mark.parametrize("N", [512, 1024])
 @pytest.mark.parametrize("info_level", [1, 2])
 @pytest.mark.parametrize("ci", range(len(V2H_CASES)))
@@ -206,11 +215,13 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, kern, monkeypatch):
     whole device state bit for bit over 6 BB steps with collisions (terminations at every sample),
     auto-resets and replanning segments."""
     env_id, over, kw = V2H_CASES[ci]
-    if kern == "v2h":
-        monkeypatch.setenv("FGX_HP", "0")
+    if kern == "hp" and (info_level < 2 or N != 512):
+        pytest.skip("FGX_HP=1 only changes the level-2 dispatch (one size)")
+    if kern != "default":
+        monkeypatch.setenv("FGX_HP", "0" if kern == "v2h" else "1")
     a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
     b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)
-    _hp_or_v2h(a, kern)
+    _hp_or_v2h(a, kern, info_level)
     np.testing.assert_array_equal(np_(a.reset(seed=5)[0]), np_(b.reset(seed=5)[0]))
     rng = np.random.default_rng(ci + 10 * info_level)
     lengths = set()
@@ -235,7 +246,7 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, kern, monkeypatch):
         assert len(lengths) > 2   # collisions ended episodes at different samples
 
 
-@pytest.mark.parametrize("kern", ["default", "v2h"])
+@pytest.mark.parametrize("kern", ["default", "v2h", "hp"])
 @pytest.mark.parametrize("env_id,over", [("fancy_ProDMP/HoleReacher-v0", None),
                                          ("fancy_ProMP/ViaPointReacher-v0",
                                           {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40)}})])
@@ -245,8 +256,8 @@ def test_v2h_nonfinite_lanes(env_id, over, kern, monkeypatch):
     state and their observation rows carry NaN cos / sin (the storing wave's placeholder, as sincos(NaN)
     in the logging kernel); bit for bit against the logging k_episode (FGX_V2=0).  Also a grid larger
     than one round of workgroups (N = 66048) and ViaPointReacher with a replanning schedule."""
-    if kern == "v2h":
-        monkeypatch.setenv("FGX_HP", "0")
+    if kern != "default":
+        monkeypatch.setenv("FGX_HP", "0" if kern == "v2h" else "1")
     for N in (768, 66048):
         a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)
         b = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over)

@@ -172,9 +172,10 @@ HELPER_CASES = [
 ]
 
 
+@pytest.mark.parametrize("hv", ["1", "2"])
 @pytest.mark.parametrize("ci", range(len(HELPER_CASES)))
-def test_jl_helper_equals_jl(ci, monkeypatch):
-    """k_episode_jl's helper form (FGX_JL_HELPER=1: one joint wave + one helper wave per workgroup,
+def test_jl_helper_equals_jl(ci, hv, monkeypatch):
+    """k_episode_jl's helper forms (FGX_JL_HELPER=1 / 2: one joint wave + one helper wave per workgroup,
     the trajectory chunks and the pairwise reduction on the helper, fgx_jl.h HLP) against the plain
     joint-lane kernel: every output and the device state bit for bit, with NaN / inf / huge
     parameters in some envs (their waves leave the fast path: the helper idles) and the split
@@ -189,7 +190,7 @@ def test_jl_helper_equals_jl(ci, monkeypatch):
         params[-1][90, :] = 3e4
     del probe
     outs = []
-    for h in ("1", "0"):
+    for h in (hv, "0"):
         monkeypatch.setenv("FGX_JL_HELPER", h)
         monkeypatch.setenv("FGX_EPISODE_KERNEL", "jl")
         env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over, random_start=False)

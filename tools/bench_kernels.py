@@ -85,8 +85,9 @@ def trajectory(env_id, N, force_valu=False, over=None, kernel=None):
     if kernel is None:
         vk = bool(over) or env_id.startswith("fancy_DMP/")
         kernel = ("k_traj_valu" if os.environ.get("FGX_TRAJ_VALU") else "k_traj_run") if vk else "k_traj_mfma"
-    print(json.dumps(dict(kernel=kernel, config=env_id, envs=N, over=str(over) if over else None,
+    print(json.dumps(dict(kernel=kernel, config=env_id, envs=N, over="replan" if over else None,
                           traj_ge=os.environ.get("FGX_TRAJ_GE"), traj_rc=os.environ.get("FGX_TRAJ_RC"),
+                          traj_nt=os.environ.get("FGX_TRAJ_NT"),
                           kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
@@ -103,12 +104,15 @@ def traj_run_scan():
         for env_id, over in cases:
             trajectory(env_id, 65536, over=over)
         os.environ.pop("FGX_TRAJ_VALU", None)
-    shapes = {"dmp": [("17", "40"), ("25", "40"), ("32", "28"), ("51", "20"), ("51", "40")],
-              "run": [("4", "200"), ("16", "200"), ("8", "100"), ("16", "48"), ("32", "40")]}
-    for env_id, over in cases:
-        for ge, rc in shapes["dmp" if "DMP/" in env_id and "ProDMP" not in env_id else "run"]:
-            os.environ["FGX_TRAJ_GE"], os.environ["FGX_TRAJ_RC"] = ge, rc
-            trajectory(env_id, 65536, over=over)
+    shapes = {"dmp": [(ge, rc) for ge in ("12", "17", "25") for rc in ("32", "40", "64")],
+              "run": [(ge, rc) for ge in ("16", "24", "32") for rc in ("32", "40", "64", "100")] + [("8", "200")]}
+    for nt in ("0", "1"):
+        os.environ["FGX_TRAJ_NT"] = nt
+        for env_id, over in cases[:2] + cases[3:]:
+            for ge, rc in shapes["dmp" if env_id.startswith("fancy_DMP/") else "run"]:
+                os.environ["FGX_TRAJ_GE"], os.environ["FGX_TRAJ_RC"] = ge, rc
+                trajectory(env_id, 65536, over=over)
+        os.environ.pop("FGX_TRAJ_NT", None)
     os.environ.pop("FGX_TRAJ_GE", None)
     os.environ.pop("FGX_TRAJ_RC", None)
 
@@ -214,7 +218,7 @@ if __name__ == "__main__":
     if "jlh" in which:   # the 8-GPU shard sizes: k_episode_jl vs its helper form, alternated three times
         for _ in range(3):
             for n in (8192, 16384, 32768):
-                for h in ("0", "1"):
+                for h in ("0", "1", "2"):
                     os.environ["FGX_EPISODE_KERNEL"] = "jl"
                     os.environ["FGX_JL_HELPER"] = h
                     episode("fancy_ProMP/LongSimpleReacher-v0", n, label=f"metric jl helper={h}")
@@ -223,7 +227,7 @@ if __name__ == "__main__":
     if "hpinfo" in which:   # config 3's verbose-2 / info-level-1 public step(): k_episode_hp vs v2h vs logging
         import os
         for lvl in (2, 1):
-            for label, env_set in (("hp", {}), ("v2h", {"FGX_HP": "0"}), ("logging", {"FGX_V2": "0"})):
+            for label, env_set in (("hp", {"FGX_HP": "1"}), ("v2h", {"FGX_HP": "0"}), ("logging", {"FGX_V2": "0"})):
                 for k in ("FGX_HP", "FGX_V2"):
                     os.environ.pop(k, None)
                 os.environ.update(env_set)
@@ -344,6 +348,11 @@ if __name__ == "__main__":
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
     if "trajrun" in which:
         traj_run_scan()
+    if "trajrun1" in which:   # one pass of each k_traj_run case (PMC runs): DMP x2, ProMP / ProDMP replanning
+        rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}
+        for env_id, over in (("fancy_DMP/LongSimpleReacher-v0", None), ("fancy_DMP/HoleReacher-v0", None),
+                             ("fancy_ProMP/LongSimpleReacher-v0", rp), ("fancy_ProDMP/HoleReacher-v0", rp)):
+            trajectory(env_id, 65536, over=over)
     if "raw" in which:   # config 1 (step-based SimpleReacher) and the other step ids at 1M envs
         for env_id in ("fancy/SimpleReacher-v0", "fancy/LongSimpleReacher-v0", "fancy/HoleReacher-v0",
                        "fancy/ViaPointReacher-v0"):
