@@ -47,7 +47,7 @@ inline int traj_run_cus() {
 template <int MP, int NL, int NB, bool V4>
 __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState s, const float* __restrict__ params,
                                                               float* __restrict__ dpos, float* __restrict__ dvel,
-                                                              int GE, int RC, int nt) {
+                                                              int GE, int RC, int nt, int sep) {
   constexpr bool SEQ = MP == MP_DMP;                   // per-joint lanes through every chunk
   using TrajT = Traj<MP, SEQ ? 1 : NL, NB>;
   extern __shared__ float4 lds_run[];
@@ -58,9 +58,14 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   float* tab = (float*)lds_run;
   const int tab_f = c.rows * c.stride;
   for (int i = t; i < tab_f; i += kTrajRunThreads) tab[i] = s.tables[i];
-  const int ESR = RC * NL + 4;                         // LDS floats per env and region (16-B aligned)
+  // LDS floats per env and region (16-B aligned): a 32-float carry area (the tail of the previous
+  // chunk that did not reach a 128-B line of the output), then the chunk's rows
+  constexpr int CA = 32;
+  const int ESR = CA + RC * NL + 4;
   float* rpos = tab + ((tab_f + 3) & ~3);
   float* rvel = rpos + GE * ESR;
+  // each array's carried tail per env ([array][env][32]), after the regions (sep: one region for both)
+  float* csave = rpos + (sep ? 1 : 2) * GE * ESR;
   const int64_t groups = (N + GE - 1) / GE;
   const int nb = NB ? NB : c.nb;
   auto lds_barrier = [] {
@@ -77,14 +82,29 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   const int parts = kTrajRunThreads / GE;
   const bool role = SEQ ? je < GE : part < parts;
 
-  // one region's pieces (rows [row0, row0 + rows) of the group's env runs) to out
-  auto store_region = [&](const float* reg, float* out, int64_t e0, int ne, int row0, int rows) __attribute__((always_inline)) {
-    const int nf = rows * NL;                          // floats per piece
+  // one region's pieces to out: of rows [row0, row0 + rows) of each env's run, the floats up to the last
+  // 128-B line boundary of the output (all of them at the run's end), after the previous chunk's carried
+  // tail; the rest (< 32 floats) is carried: copied in front of the region's next rows.  Every line of the
+  // output but a run's first and last is then written whole by one piece (tools/wbench.hip: 800-B pieces
+  // 4.1-4.7 TB/s aligned against 3.3-4.4 unaligned, profiles/r05_s11_wbench.jsonl)
+  auto store_region = [&](float* reg, float* out, int64_t e0, int ne, int row0, int rows, int arr) __attribute__((always_inline)) {
+    const bool last = row0 + rows >= T;
     for (int j = wave; j < ne; j += kTrajRunThreads / 64) {
-      gchar* base = uniform_ptr(out + ((e0 + j) * T + row0) * NL);
-      const float* src = reg + j * ESR;
+      const int64_t g0 = (e0 + j) * (int64_t)T * NL;   // the run's first float in out
+      // (nt bit 1, A/B: pieces end on rows, as before)
+      auto aligned_end = [&](int r) { return (nt & 2) ? r * NL : r * NL - (int)((g0 + (int64_t)r * NL) & 31); };
+      const int fs = row0 == 0 ? 0 : aligned_end(row0);
+      const int fe = last ? T * NL : aligned_end(row0 + rows);
+      gchar* base = uniform_ptr(out + g0 + fs);
+      float* src = reg + j * ESR + CA + (fs - row0 * NL);
+      const int nf = fe - fs;
+      float* cs = csave + (arr * GE + j) * CA;
+      {   // the previous chunk's tail of this array in front of the rows (this wave saved it)
+        const int ncp = row0 * NL - fs;
+        for (int f = lane; f < ncp; f += 64) src[f] = cs[f];
+      }
       if constexpr (V4) {
-        if (nt) {   // (A/B: streaming stores)
+        if (nt & 1) {   // streaming stores
           for (int ch = lane; ch < nf / 4; ch += 64)
             __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(src + 4 * ch),
                                         (__attribute__((address_space(1))) f32x4*)(base + 16u * (uint32_t)ch));
@@ -94,6 +114,11 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
         }
       } else {
         for (int f = lane; f < nf; f += 64) *(__attribute__((address_space(1))) float*)(base + 4u * (uint32_t)f) = src[f];
+      }
+      if (!last) {   // the new tail (this wave's LDS ops run in order: the piece was read first)
+        const int nc = (row0 + rows) * NL - fe;
+        const float* cb = reg + j * ESR + CA + (fe - row0 * NL);
+        for (int f = lane; f < nc; f += 64) cs[f] = cb[f];
       }
     }
   };
@@ -125,101 +150,137 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
     }
     for (int row0 = 0; row0 < T; row0 += RC) {
       const int rows = min(RC, T - row0);
-      if (act) {
-        float pos[SEQ ? 1 : NL], vel[SEQ ? 1 : NL];
-        if constexpr (SEQ) {
-          float* dp = rpos + je * ESR + dl;
-          float* dv = rvel + je * ESR + dl;
+      if constexpr (SEQ) {
+        if (act) {
+          float pos[1], vel[1];
+          float* dp = rpos + je * ESR + CA + dl;
+          float* dv = rvel + je * ESR + CA + dl;
           for (int k = row0; k < row0 + rows; ++k) {
             tg.template at_rows<false>(c, k, tab + (size_t)(s0 + k + 1) * str, pos, vel);
             dp[(k - row0) * NL] = pos[0];
             dv[(k - row0) * NL] = vel[0];
           }
-        } else {
+        }
+        lds_barrier();
+        store_region(rpos, dpos, e0, ne, row0, rows, 0);
+        store_region(rvel, dvel, e0, ne, row0, rows, 1);
+        lds_barrier();   // every wave's region reads done before the next chunk overwrites it
+      } else {
+        // WHICH 0: positions and velocities into their regions; 1 / 2 (sep): positions / velocities
+        // into the one region (the other half of at_rows is dead code)
+        auto comp = [&](auto which) __attribute__((always_inline)) {
+          constexpr int W = decltype(which)::value;
+          if (!act) return;
+          float pos[NL], vel[NL];
           const int rs = (rows + parts - 1) / parts;   // rows per lane
           const int kb = row0 + part * rs, kend = min(kb + rs, row0 + rows);
-          if (kb < kend) {
-            int ka = kb;
-            if constexpr (MP == MP_PROMP) {
-              // re-seed the look-ahead at row ka (a run starting at the last sample starts one early)
-              if (kb == T - 1 && kb > 0) ka = kb - 1;
-              tg.T = T - ka;
-              const float* r1 = tab + (size_t)(s0 + ka + 1) * str;
-              if constexpr (TrajT::PK) {
+          if (kb >= kend) return;
+          int ka = kb;
+          if constexpr (MP == MP_PROMP) {
+            // re-seed the look-ahead at row ka (a run starting at the last sample starts one early)
+            if (kb == T - 1 && kb > 0) ka = kb - 1;
+            tg.T = T - ka;
+            const float* r1 = tab + (size_t)(s0 + ka + 1) * str;
+            if constexpr (TrajT::PK) {
 #pragma unroll
-                for (int p = 0; p < TrajT::NLP; ++p) { tg.cur2[p] = tg.chain2(r1, tg.wp[p]); tg.vprev2[p] = (f32x2)0.0f; }
-              } else {
+              for (int p = 0; p < TrajT::NLP; ++p) { tg.cur2[p] = tg.chain2(r1, tg.wp[p]); tg.vprev2[p] = (f32x2)0.0f; }
+            } else {
 #pragma unroll
-                for (int d = 0; d < NL; ++d) { tg.cur[d] = tg.chain(r1, tg.w[d]); tg.vprev[d] = 0.0f; }
-              }
+              for (int d = 0; d < NL; ++d) { tg.cur[d] = tg.chain(r1, tg.w[d]); tg.vprev[d] = 0.0f; }
             }
-            float* dp = rpos + je * ESR;
-            float* dv = rvel + je * ESR;
-            for (int k = ka; k < kend; ++k) {
-              tg.template at_rows<false>(c, MP == MP_PROMP ? k - ka : k, tab + (size_t)(s0 + k + 1) * str, pos, vel);
-              if (k >= kb) {
+          }
+          float* dp = rpos + je * ESR + CA;
+          float* dv = rvel + je * ESR + CA;
+          for (int k = ka; k < kend; ++k) {
+            tg.template at_rows<false>(c, MP == MP_PROMP ? k - ka : k, tab + (size_t)(s0 + k + 1) * str, pos, vel);
+            if (k >= kb) {
 #pragma unroll
-                for (int d = 0; d < NL; ++d) {
+              for (int d = 0; d < NL; ++d) {
+                if constexpr (W == 0) {
                   dp[(k - row0) * NL + d] = pos[d];
                   dv[(k - row0) * NL + d] = vel[d];
+                } else {
+                  dp[(k - row0) * NL + d] = W == 1 ? pos[d] : vel[d];
                 }
               }
             }
           }
+        };
+        if (!sep) {
+          comp(std::integral_constant<int, 0>{});
+          lds_barrier();
+          store_region(rpos, dpos, e0, ne, row0, rows, 0);
+          store_region(rvel, dvel, e0, ne, row0, rows, 1);
+          lds_barrier();
+        } else {
+          comp(std::integral_constant<int, 1>{});
+          lds_barrier();
+          store_region(rpos, dpos, e0, ne, row0, rows, 0);
+          lds_barrier();
+          comp(std::integral_constant<int, 2>{});
+          lds_barrier();
+          store_region(rpos, dvel, e0, ne, row0, rows, 1);
+          lds_barrier();
         }
       }
-      lds_barrier();
-      store_region(rpos, dpos, e0, ne, row0, rows);
-      store_region(rvel, dvel, e0, ne, row0, rows);
-      lds_barrier();   // every wave's region reads done before the next chunk overwrites it
     }
   }
 }
 
 // workgroup shape of k_traj_run: GE envs per group, RC rows per chunk (RC >= T: whole runs), nt:
-// streaming stores.  Chosen from the A/B at 65536 envs, T = 200, 5 links
-// (profiles/r05_s10_traj_hpinfo.jsonl, us per launch):
-//   * ProMP (replanning): whole runs of 8 envs (two workgroups per CU) 102 us, 5.2 TB/s;
-//   * ProDMP (replanning, a 402-row table in LDS): 16 envs x 64 rows with streaming stores 151 us
-//     (whole runs of 8 envs 303-313 us: the table leaves room for one workgroup per CU);
-//   * DMP: one wave of joint lanes (64 / dof envs) x 40 rows 167 us (12 x 32 / 64: 174 / 193;
-//     17 / 25 envs: 175-185; streaming stores no better).
-// FGX_TRAJ_GE / FGX_TRAJ_RC / FGX_TRAJ_NT=0|1 override (A/B).
+// streaming stores, sep: positions then velocities through one region.  Chosen from the A/B sweeps at
+// 65536 envs, T = 200, 5 links (profiles/r05_s10_traj_hpinfo.jsonl, r05_s11_traj_sweep.jsonl, us per
+// launch; sessions differ by up to 15%):
+//   * ProMP (replanning): whole runs of 8 envs, one region: 105.6 us (both regions 102-122 us);
+//   * ProDMP (replanning, a 402-row table in LDS): whole runs of 12 envs, one region, streaming
+//     stores: 128.9 us (16 envs x 64 rows, two regions: 151-155; whole runs, two regions: 192-315);
+//   * DMP (sequential per joint): one wave of joint lanes (64 / dof envs) x 40 rows, streaming
+//     stores: 162-167 us (regular stores 167-190; 12 x 32 / 64 rows: 165-205; 17 / 25 envs: 175-218;
+//     pieces ending on 128-B lines or on rows: within the sessions' noise, r05_s12_traj_sweep.jsonl).
+// FGX_TRAJ_GE / _RC / _NT=0|1 / _SEP=0|1 / _ALIGN=0 override (A/B).
 struct TrajRunShape {
-  int GE, RC, nt;
+  int GE, RC, nt, sep;
   size_t lds;
 };
-inline size_t traj_run_lds(const DevCfg& c, int GE, int RC) {
-  return (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4 + 2 * (size_t)GE * ((size_t)RC * c.nl + 4) * 4;
+// sep: positions, then velocities through one region (ProMP / ProDMP)
+inline size_t traj_run_lds(const DevCfg& c, int GE, int RC, int sep = 0) {
+  return (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4 + (sep ? 1 : 2) * (size_t)GE * (32 + (size_t)RC * c.nl + 4) * 4 +
+         2 * (size_t)GE * 32 * 4;
 }
 inline TrajRunShape traj_run_shape(const DevCfg& c) {
   const int nl = c.nl, T = c.T;
   const size_t budget = 80 * 1024;   // two workgroups per CU
-  int GE, RC, nt = 0;
-  // RC * nl a multiple of 4 (whole 16-B chunks per piece)
-  auto rc_align = [&](int rc) { while (rc > 4 && (rc * nl) % 4) --rc; return rc; };
+  int GE, RC, nt = 0, sep = 0;
   if (c.mp == MP_DMP) {
     GE = 64 / nl;
-    RC = rc_align(std::min(T, 40));
-  } else if (c.mp == MP_PRODMP) {
-    GE = 16;
-    RC = rc_align(std::min(T, 64));
+    RC = std::min(T, 40);
     nt = 1;
-  } else {
-    GE = 32;
-    while (GE > 1 && traj_run_lds(c, GE, T) > budget) GE >>= 1;
+  } else {   // whole runs, positions then velocities through one region
+    sep = 1;
+    GE = c.mp == MP_PRODMP ? 12 : 8;
+    nt = c.mp == MP_PRODMP ? 1 : 0;
+    while (GE > 1 && traj_run_lds(c, GE, T, 1) > budget) --GE;
     RC = T;
-    if (traj_run_lds(c, GE, T) > budget) {   // a run too long for the region: chunks
-      const size_t per = budget > traj_run_lds(c, GE, 0) ? (budget - traj_run_lds(c, GE, 0)) / (2 * (size_t)GE * 4) : 0;
-      RC = rc_align(std::max(4, (int)std::min<size_t>((size_t)T, per / nl)));
+    if (traj_run_lds(c, GE, T, 1) > budget) {   // a run too long for the region: chunks
+      const size_t fixed = traj_run_lds(c, GE, 0, 1);
+      const size_t per = budget > fixed ? (budget - fixed) / ((size_t)GE * 4) : 0;
+      RC = std::max(4, (int)std::min<size_t>((size_t)T, per / nl));
     }
   }
   if (const char* v = std::getenv("FGX_TRAJ_GE")) GE = std::max(1, std::min(kTrajRunThreads, std::atoi(v)));
   if (c.mp == MP_DMP) GE = std::min(GE, kTrajRunThreads / nl);
   if (const char* v = std::getenv("FGX_TRAJ_RC")) RC = std::max(1, std::min(T, std::atoi(v)));
   if (const char* v = std::getenv("FGX_TRAJ_NT")) nt = v[0] == '1';
+  if (const char* v = std::getenv("FGX_TRAJ_ALIGN"))
+    if (v[0] == '0') nt |= 2;
+  if (const char* v = std::getenv("FGX_TRAJ_SEP")) sep = v[0] == '1' && c.mp != MP_DMP;
   RC = std::min(RC, T);
-  return {GE, RC, nt, traj_run_lds(c, GE, RC)};
+  if (RC < T) {   // a chunk spans at least one 128-B line (the carry stays below 32 floats); whole 16-B chunks
+    RC = std::max(RC, (32 + nl - 1) / nl);
+    while ((RC * nl) % 4 && RC < T) ++RC;
+    if (RC < T && (RC * nl) % 4) RC = T;
+  }
+  return {GE, RC, nt, sep, traj_run_lds(c, GE, RC, sep)};
 }
 
 // 0: launched; 1: not applicable (the caller runs k_traj_valu); 2: launch error
@@ -239,7 +300,7 @@ inline int launch_traj_run(const DevCfg& c, const DevState& s, const float* para
 #define RUN(MPV, NBV, V4V)                                                                                      \
   launch_lds((const void*)k_traj_run<MPV, NL, NBV, V4V>, sh.lds, [&] {                                        \
     hipLaunchKernelGGL((k_traj_run<MPV, NL, NBV, V4V>), grid, block, sh.lds, stream, c, s, params, dpos, dvel, \
-                       sh.GE, sh.RC, nt);                                                                     \
+                       sh.GE, sh.RC, nt, sh.sep);                                                             \
   })
 #define BY_V4(MPV, NBV) \
   if (v4) RUN(MPV, NBV, true); else RUN(MPV, NBV, false)

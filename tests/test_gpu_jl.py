@@ -205,3 +205,4 @@ def test_jl_helper_equals_jl(ci, hv, monkeypatch):
             out += list(_state(env).values())
         outs.append(out)
     _same(outs[0], outs[1])
+

@@ -34,7 +34,7 @@ CASES = [
 
 
 def _traj(env_id, over, kw, N, n_bb, monkeypatch, env_vars):
-    for k in ("FGX_TRAJ_VALU", "FGX_TRAJ_GE", "FGX_TRAJ_RC"):
+    for k in ("FGX_TRAJ_VALU", "FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env_vars.items():
         monkeypatch.setenv(k, v)
@@ -53,7 +53,9 @@ def _traj(env_id, over, kw, N, n_bb, monkeypatch, env_vars):
 def test_traj_run_equals_valu(ci, monkeypatch):
     env_id, over, kw, N, n_bb = CASES[ci]
     _, _, rp, rv = _traj(env_id, over, kw, N, n_bb, monkeypatch, {"FGX_TRAJ_VALU": "1"})
-    for vars_ in ({}, {"FGX_TRAJ_RC": "36"}, {"FGX_TRAJ_GE": "3", "FGX_TRAJ_RC": "17"}):
+    for vars_ in ({}, {"FGX_TRAJ_RC": "36"}, {"FGX_TRAJ_GE": "3", "FGX_TRAJ_RC": "17"},
+                  {"FGX_TRAJ_SEP": "1", "FGX_TRAJ_NT": "1", "FGX_TRAJ_GE": "5"},
+                  {"FGX_TRAJ_SEP": "0", "FGX_TRAJ_RC": "64", "FGX_TRAJ_ALIGN": "0"}):
         _, _, p, v = _traj(env_id, over, kw, N, n_bb, monkeypatch, vars_)
         assert p.shape == rp.shape
         np.testing.assert_array_equal(p.view(np.uint32), rp.view(np.uint32), err_msg=str(vars_))

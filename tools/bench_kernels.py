@@ -87,7 +87,8 @@ def trajectory(env_id, N, force_valu=False, over=None, kernel=None):
         kernel = ("k_traj_valu" if os.environ.get("FGX_TRAJ_VALU") else "k_traj_run") if vk else "k_traj_mfma"
     print(json.dumps(dict(kernel=kernel, config=env_id, envs=N, over="replan" if over else None,
                           traj_ge=os.environ.get("FGX_TRAJ_GE"), traj_rc=os.environ.get("FGX_TRAJ_RC"),
-                          traj_nt=os.environ.get("FGX_TRAJ_NT"),
+                          traj_nt=os.environ.get("FGX_TRAJ_NT"), traj_sep=os.environ.get("FGX_TRAJ_SEP"),
+                          traj_align=os.environ.get("FGX_TRAJ_ALIGN"),
                           kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
@@ -104,17 +105,26 @@ def traj_run_scan():
         for env_id, over in cases:
             trajectory(env_id, 65536, over=over)
         os.environ.pop("FGX_TRAJ_VALU", None)
-    shapes = {"dmp": [(ge, rc) for ge in ("12", "17", "25") for rc in ("32", "40", "64")],
-              "run": [(ge, rc) for ge in ("16", "24", "32") for rc in ("32", "40", "64", "100")] + [("8", "200")]}
-    for nt in ("0", "1"):
-        os.environ["FGX_TRAJ_NT"] = nt
-        for env_id, over in cases[:2] + cases[3:]:
-            for ge, rc in shapes["dmp" if env_id.startswith("fancy_DMP/") else "run"]:
-                os.environ["FGX_TRAJ_GE"], os.environ["FGX_TRAJ_RC"] = ge, rc
-                trajectory(env_id, 65536, over=over)
-        os.environ.pop("FGX_TRAJ_NT", None)
-    os.environ.pop("FGX_TRAJ_GE", None)
-    os.environ.pop("FGX_TRAJ_RC", None)
+    def run(env_id, over, **kv):
+        for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN"):
+            os.environ.pop(k, None)
+        os.environ.update({"FGX_TRAJ_" + k: v for k, v in kv.items()})
+        trajectory(env_id, 65536, over=over)
+    for env_id, over in cases[:2]:   # DMP: chunk rows, 128-B aligned pieces or not, store kind
+        for rc in ("32", "40", "64"):
+            for al in ("1", "0"):
+                for nt in ("0", "1"):
+                    run(env_id, over, GE="12", RC=rc, ALIGN=al, NT=nt)
+    for env_id, over in cases[2:]:   # ProMP / ProDMP: whole runs through one region, group size, store kind
+        for ge in ("6", "8", "10", "12", "16"):
+            for nt in ("0", "1"):
+                run(env_id, over, GE=ge, RC="200", SEP="1", NT=nt)
+        run(env_id, over, GE="16", RC="64", SEP="0", NT="1")
+        run(env_id, over, GE="16", RC="64", SEP="0", NT="1", ALIGN="0")
+    for env_id, over in cases:   # the defaults again, end of session
+        run(env_id, over)
+    for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN"):
+        os.environ.pop(k, None)
 
 
 def mfma_ab(env_id="fancy_ProMP/LongSimpleReacher-v0", N=65536, reps=20):

@@ -49,7 +49,10 @@ fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 kern = env.episode_kernel()
 JL = kern in ("k_episode_jl", "k_episode_jl_pc")
 wpb = 8 if kern == "k_episode_jl_pc" else 4   # stamped waves per workgroup (joint waves [+ producers])
-if JL:
+import os  # noqa: E402
+if JL and os.environ.get("FGX_JL_HELPER", "0") in ("1", "2"):   # one stamped joint wave per workgroup
+    W = (N + 64 // env._eng.cfg.n_links - 1) // (64 // env._eng.cfg.n_links)
+elif JL:
     epb = 4 * (64 // env._eng.cfg.n_links)
     W = (N + epb - 1) // epb * wpb
 else:

@@ -26,6 +26,32 @@ __global__ void k_piece(float* out, long long nenv, int run, int piece, int wave
     }
 }
 
+// the same pieces with their boundaries moved to 128-B lines of the output (the run's ends excepted):
+// every line but a run's first / last is written whole by one piece
+template <int ALIGN>
+__global__ void k_piece_aligned(float* out, long long nenv, int run, int piece, int waves_per_group) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const long long gw = (long long)blockIdx.x * wpb + w;
+  const long long grp = gw / waves_per_group;
+  const int sub = gw % waves_per_group;
+  const long long e0 = grp * 32;
+  if (e0 >= nenv) return;
+  const int npieces = run / piece;
+  const f32x4 v = {1.0f, 2.0f, 3.0f, 4.0f};
+  for (int k = sub; k < npieces; k += waves_per_group)
+    for (int je = 0; je < 32; ++je) {
+      const long long S = (e0 + je) * (long long)run;
+      auto bound = [&](int kk) -> long long {
+        if (kk <= 0) return S;
+        if (kk >= npieces) return S + run;
+        return ALIGN ? (S + (long long)kk * piece + 127) & ~127LL : S + (long long)kk * piece;
+      };
+      const long long b0 = bound(k), b1 = bound(k + 1);
+      for (long long off = b0 + 16 * lane; off < b1; off += 16 * 64) *(f32x4*)((char*)out + off) = v;
+    }
+}
+
 template <int NT>
 __global__ void k_linear(float* out, long long nenv, int run, int waves_per_group) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -70,6 +96,8 @@ int main() {
         if (linear == 1) hipLaunchKernelGGL(k_linear<0>, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv, run, wpg);
         else if (linear == 2) hipLaunchKernelGGL(k_linear<1>, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv, run, wpg);
         else if (linear == 3) hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv * run / 16);
+        else if (linear == 4) hipLaunchKernelGGL(k_piece_aligned<1>, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv, run, piece, wpg);
+        else if (linear == 5) hipLaunchKernelGGL(k_piece_aligned<0>, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv, run, piece, wpg);
         else hipLaunchKernelGGL(k_piece, dim3(blocks), dim3(64 * wpb), 0, 0, buf[i], nenv, run, piece, wpg);
       }
       hipEventRecord(b);
@@ -90,5 +118,11 @@ int main() {
   timeit("fill_gridstride", 0, 1, 16, 3);  // 128 x 1024
   timeit("piece", 4000, 1, 4, 0);
   timeit("piece", 4000, 8, 8, 0);
+  for (int pc : {400, 800}) {   // (whole 16-B chunks per piece)
+    timeit("piece_per_env", pc, 8, 8, 5);
+    timeit("piece_aligned", pc, 8, 8, 4);
+    timeit("piece_per_env", pc, 1, 4, 5);
+    timeit("piece_aligned", pc, 1, 4, 4);
+  }
   return 0;
 }
