@@ -379,9 +379,10 @@ class BlackBoxVectorEnv:
     def episode_kernel(self, info_level=None):
         """Name of the HIP kernel step() launches (fgx_episode_kernel): k_episode, k_episode_jp,
         k_episode_ws, k_episode_jl, k_episode_w2, k_episode_pair, k_episode_v2, k_episode_v2h or k_episode_hp
-        (HoleReacher without per-step arrays); all nine produce bit-identical results.  The launch takes the logging k_episode (or, for SimpleReacher + PD, k_episode_v2;
-        for the direct envs at a multiple of 256 envs, k_episode_v2h) whenever
-        some per-step array is written: info_level >= 1, or a reward_aggregation that reads step_rewards."""
+        (HoleReacher up to info_level 1); all nine produce bit-identical results.  Whenever some per-step
+        array is written (info_level >= 1, or a reward_aggregation that reads step_rewards) the launch
+        takes k_episode_hp (HoleReacher below the verbose-2 rows), k_episode_v2 (SimpleReacher + PD),
+        k_episode_v2h (the direct envs at a multiple of 256 envs) or the logging k_episode."""
         lvl = self.info_level if info_level is None else int(info_level)
         if self._needs_step_rewards():
             lvl = max(lvl, 1)

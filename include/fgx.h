@@ -269,10 +269,11 @@ int fgx_get_tables(void* handle, float* out, void* stream);
  * (HoleReacher, two lanes per env), 6 = k_episode_v2 (SimpleReacher + PD with per-step arrays: dynamics
  * and observation-trigonometry waves side by side), 7 = k_episode_v2h (HoleReacher / ViaPointReacher with
  * per-step arrays, n_envs % 256 == 0: the logging body beside a wave that stores its rows), 8 = k_episode_hp
- * (HoleReacher without per-step arrays: a producer wave of dynamics feeding two consumer waves of FK /
- * collision / reward through LDS, + k_hp_finish for the epilogue); negative on error.  info_level >= 1
- * means some per-step output pointer is given (the launch then runs the logging k_episode, k_episode_v2
- * or k_episode_v2h, as it does for a config with valid_flags).  All nine give
+ * (HoleReacher up to info level 1: a producer wave of dynamics feeding two consumer waves of FK /
+ * collision / reward / per-step rows through LDS, + k_hp_finish for the epilogue); negative on error.
+ * info_level >= 1 means some per-step output pointer is given (the launch then runs k_episode_hp, the
+ * logging k_episode, k_episode_v2 or k_episode_v2h, as it does for a config with valid_flags; 2: the
+ * verbose-2 rows, planned positions and step observations included).  All nine give
  * bit-identical results; the choice follows measured speed (fgx_dispatch.h, fgx_hp.h). */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 
