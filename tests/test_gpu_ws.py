@@ -63,8 +63,9 @@ def test_episode_kernel_selection():
              ("fancy_ProDMP/SimpleReacher-v0", rp, 8192, 0, "k_episode_jl"),         # config 5 shard
              ("fancy_ProMP/SimpleReacher-v0", None, 65536, 0, "k_episode_jl"),       # 2 links: every size
              ("fancy_ProDMP/HoleReacher-v0", None, 4096, 0, "k_episode_hp"),     # producer / consumer pipeline
-             ("fancy_ProDMP/HoleReacher-v0", None, 4096, 1, "k_episode_v2h"),     # per-step info, whole workgroups
-             ("fancy_ProDMP/HoleReacher-v0", None, 4000, 1, "k_episode")]          # per-step info, a partial one
+             ("fancy_ProDMP/HoleReacher-v0", None, 4000, 1, "k_episode_hp"),     # info level 1: its rows instantiation
+             ("fancy_ProDMP/HoleReacher-v0", None, 4096, 2, "k_episode_v2h"),    # verbose-2 rows, whole workgroups
+             ("fancy_ProDMP/HoleReacher-v0", None, 4000, 2, "k_episode")]         # verbose-2 rows, a partial one
     for env_id, over, N, lvl, want in cases:
         env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over)
         assert kernel_is(env.episode_kernel(lvl), want), (env_id, N, lvl)

@@ -211,6 +211,9 @@ if __name__ == "__main__":
                 env_kwargs={"allow_wall_collision": True})
         episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3 allow_self_collision", reps=5,
                 env_kwargs={"allow_self_collision": True})
+    if "hp3" in which:   # config 3 with the default kernel (A/B of library builds)
+        for n in (65536, 32768):
+            episode("fancy_ProDMP/HoleReacher-v0", n, label="config3", reps=10)
     if "hp" in which:   # config 3: k_episode_hp (both workgroup shapes) against k_episode / k_episode_pair
         import os
         for n in (65536, 32768, 16384, 131072):
