@@ -57,11 +57,12 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   const int str = TrajT::KS ? TrajT::KS : c.stride;
   float* tab = (float*)lds_run;
   const int tab_f = c.rows * c.stride;
-  for (int i = t; i < tab_f; i += kTrajRunThreads) tab[i] = s.tables[i];
+  const int nthr = blockDim.x;   // 64 .. kTrajRunThreads (host: DMP one wave, else 256)
+  for (int i = t; i < tab_f; i += nthr) tab[i] = s.tables[i];
   // LDS floats per env and region (16-B aligned): a 32-float carry area (the tail of the previous
   // chunk that did not reach a 128-B line of the output), then the chunk's rows
   constexpr int CA = 32;
-  const int ESR = CA + RC * NL + 4;
+  const int ESR = CA + RC * NL;
   float* rpos = tab + ((tab_f + 3) & ~3);
   float* rvel = rpos + GE * ESR;
   // each array's carried tail per env ([array][env][32]), after the regions (sep: one region for both)
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   const int je = SEQ ? t / NL : t % GE;               // env of the group
   const int dl = SEQ ? t - je * NL : 0;               // DMP: the lane's joint
   const int part = SEQ ? 0 : t / GE;                  // ProMP / ProDMP: the lane's run of rows
-  const int parts = kTrajRunThreads / GE;
+  const int parts = nthr / GE;
   const bool role = SEQ ? je < GE : part < parts;
 
   // one region's pieces to out: of rows [row0, row0 + rows) of each env's run, the floats up to the last
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   // 4.1-4.7 TB/s aligned against 3.3-4.4 unaligned, profiles/r05_s11_wbench.jsonl)
   auto store_region = [&](float* reg, float* out, int64_t e0, int ne, int row0, int rows, int arr) __attribute__((always_inline)) {
     const bool last = row0 + rows >= T;
-    for (int j = wave; j < ne; j += kTrajRunThreads / 64) {
+    for (int j = wave; j < ne; j += nthr >> 6) {
       const int64_t g0 = (e0 + j) * (int64_t)T * NL;   // the run's first float in out
       // (nt bit 1, A/B: pieces end on rows, as before)
       auto aligned_end = [&](int r) { return (nt & 2) ? r * NL : r * NL - (int)((g0 + (int64_t)r * NL) & 31); };
@@ -237,14 +238,16 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
 //   * DMP (sequential per joint): one wave of joint lanes (64 / dof envs) x 40 rows, streaming
 //     stores: 162-167 us (regular stores 167-190; 12 x 32 / 64 rows: 165-205; 17 / 25 envs: 175-218;
 //     pieces ending on 128-B lines or on rows: within the sessions' noise, r05_s12_traj_sweep.jsonl).
-// FGX_TRAJ_GE / _RC / _NT=0|1 / _SEP=0|1 / _ALIGN=0 override (A/B).
+//     DMP is sensitive to the workgroups per CU (LDS-bound; its joint lanes fill wave 0, every wave
+//     stores): four per CU 272 us, five 169-183 us, one-wave workgroups 480 us (r05_s15..s17_dmp_shapes).
+// FGX_TRAJ_GE / _RC / _NT=0|1 / _SEP=0|1 / _ALIGN=0 / _THREADS / _PERCU override (A/B).
 struct TrajRunShape {
-  int GE, RC, nt, sep;
+  int GE, RC, nt, sep, threads, per_cu;
   size_t lds;
 };
 // sep: positions, then velocities through one region (ProMP / ProDMP)
 inline size_t traj_run_lds(const DevCfg& c, int GE, int RC, int sep = 0) {
-  return (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4 + (sep ? 1 : 2) * (size_t)GE * (32 + (size_t)RC * c.nl + 4) * 4 +
+  return (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4 + (sep ? 1 : 2) * (size_t)GE * (32 + (size_t)RC * c.nl) * 4 +
          2 * (size_t)GE * 32 * 4;
 }
 inline TrajRunShape traj_run_shape(const DevCfg& c) {
@@ -268,7 +271,14 @@ inline TrajRunShape traj_run_shape(const DevCfg& c) {
     }
   }
   if (const char* v = std::getenv("FGX_TRAJ_GE")) GE = std::max(1, std::min(kTrajRunThreads, std::atoi(v)));
-  if (c.mp == MP_DMP) GE = std::min(GE, kTrajRunThreads / nl);
+  int threads = kTrajRunThreads;   // (DMP: the joint lanes on wave 0; every wave stores)
+  if (const char* v = std::getenv("FGX_TRAJ_THREADS")) threads = std::max(1, std::min(4, std::atoi(v) / 64)) * 64;
+  if (c.mp == MP_DMP) {
+    GE = std::min(GE, kTrajRunThreads / nl);
+    threads = std::max(threads, (GE * nl + 63) / 64 * 64);
+  } else {
+    GE = std::min(GE, threads);
+  }
   if (const char* v = std::getenv("FGX_TRAJ_RC")) RC = std::max(1, std::min(T, std::atoi(v)));
   if (const char* v = std::getenv("FGX_TRAJ_NT")) nt = v[0] == '1';
   if (const char* v = std::getenv("FGX_TRAJ_ALIGN"))
@@ -280,7 +290,10 @@ inline TrajRunShape traj_run_shape(const DevCfg& c) {
     while ((RC * nl) % 4 && RC < T) ++RC;
     if (RC < T && (RC * nl) % 4) RC = T;
   }
-  return {GE, RC, nt, sep, traj_run_lds(c, GE, RC, sep)};
+  const size_t lds = traj_run_lds(c, GE, RC, sep);
+  int per_cu = (int)std::max<size_t>(1, std::min<size_t>(16, (160 * 1024) / std::max<size_t>(lds, 1)));
+  if (const char* v = std::getenv("FGX_TRAJ_PERCU")) per_cu = std::max(1, std::min(per_cu, std::atoi(v)));
+  return {GE, RC, nt, sep, threads, per_cu, lds};
 }
 
 // 0: launched; 1: not applicable (the caller runs k_traj_valu); 2: launch error
@@ -294,9 +307,8 @@ inline int launch_traj_run(const DevCfg& c, const DevState& s, const float* para
   const bool v4 = ((c.T * NL) % 4) == 0 && ((sh.RC * NL) % 4) == 0 && (((uintptr_t)dpos | (uintptr_t)dvel) & 15) == 0;
   const int64_t groups = (c.N + sh.GE - 1) / sh.GE;
   const int nt = sh.nt;
-  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(sh.lds, 1)));
-  const int blocks = (int)std::min<int64_t>(groups, (int64_t)traj_run_cus() * per_cu);
-  const dim3 grid(blocks), block(kTrajRunThreads);
+  const int blocks = (int)std::min<int64_t>(groups, (int64_t)traj_run_cus() * sh.per_cu);
+  const dim3 grid(blocks), block(sh.threads);
 #define RUN(MPV, NBV, V4V)                                                                                      \
   launch_lds((const void*)k_traj_run<MPV, NL, NBV, V4V>, sh.lds, [&] {                                        \
     hipLaunchKernelGGL((k_traj_run<MPV, NL, NBV, V4V>), grid, block, sh.lds, stream, c, s, params, dpos, dvel, \

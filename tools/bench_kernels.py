@@ -88,7 +88,7 @@ def trajectory(env_id, N, force_valu=False, over=None, kernel=None):
     print(json.dumps(dict(kernel=kernel, config=env_id, envs=N, over="replan" if over else None,
                           traj_ge=os.environ.get("FGX_TRAJ_GE"), traj_rc=os.environ.get("FGX_TRAJ_RC"),
                           traj_nt=os.environ.get("FGX_TRAJ_NT"), traj_sep=os.environ.get("FGX_TRAJ_SEP"),
-                          traj_align=os.environ.get("FGX_TRAJ_ALIGN"),
+                          traj_align=os.environ.get("FGX_TRAJ_ALIGN"), traj_threads=os.environ.get("FGX_TRAJ_THREADS"),
                           kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
@@ -361,6 +361,17 @@ if __name__ == "__main__":
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
     if "trajrun" in which:
         traj_run_scan()
+    if "dmp" in which:   # DMP trajectory: the default shape against explicit ones
+        for kv in ({}, {"FGX_TRAJ_GE": "6"}, {"FGX_TRAJ_GE": "8"}, {"FGX_TRAJ_GE": "10"},
+                   {"FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "6", "FGX_TRAJ_RC": "64"}, {"FGX_TRAJ_GE": "4"},
+                   {"FGX_TRAJ_GE": "8", "FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "6", "FGX_TRAJ_NT": "0"},
+                   {"FGX_TRAJ_THREADS": "128", "FGX_TRAJ_GE": "6"}, {}):
+            for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN", "FGX_TRAJ_THREADS"):
+                os.environ.pop(k, None)
+            os.environ.update(kv)
+            trajectory("fancy_DMP/LongSimpleReacher-v0", 65536)
+        for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN"):
+            os.environ.pop(k, None)
     if "trajrun1" in which:   # one pass of each k_traj_run case (PMC runs): DMP x2, ProMP / ProDMP replanning
         rp = {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(200)}}
         for env_id, over in (("fancy_DMP/LongSimpleReacher-v0", None), ("fancy_DMP/HoleReacher-v0", None),
