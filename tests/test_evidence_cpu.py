@@ -1,6 +1,6 @@
 """The committed measurement evidence is self-consistent (no GPU): the bench line's roofline can be
 recomputed from profiles/pmc_summary.json, whose entries are of the library build in this tree, and
-tools/pmc_summary.py rebuilds the summary from the committed counter CSVs (profiles/r04_pmc/)."""
+tools/pmc_summary.py rebuilds the summary from the committed counter CSVs (profiles/r05_pmc/)."""
 import json
 import os
 import subprocess
@@ -13,8 +13,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from fancy_gym_crowd_amd import _build  # noqa: E402
 
-BENCH_LINE = os.path.join(ROOT, "profiles", "r04_bench_n1_final.json")
-KERNEL_STATS = os.path.join(ROOT, "profiles", "r04_kernel_stats_bench_final.csv")
+BENCH_LINE = os.path.join(ROOT, "profiles", "r05_bench_n1_final.json")
+KERNEL_STATS = os.path.join(ROOT, "profiles", "r05_kernel_stats_bench_final.csv")
 
 
 def _line():
@@ -26,7 +26,7 @@ def _current_or_skip(ids):
     """evidence of another build (sources changed since the PMC passes): nothing to check yet"""
     if ids != {_build.source_hash()}:
         pytest.skip(f"profiles are of build(s) {sorted(ids)}, the sources are {_build.source_hash()}: "
-                    "re-run tools/gpu_pmc_r03.sh and tools/gpu_final_r04.sh")
+                    "re-run tools/gpu_pmc_r03.sh and tools/gpu_final_r05.sh")
 
 
 def test_pmc_summary_is_of_this_tree():
@@ -66,7 +66,7 @@ def test_bench_roofline_recomputes_from_profiles():
 def test_pmc_summary_rebuilds_from_committed_csvs(tmp_path):
     out = tmp_path / "s.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
-                    os.path.join(ROOT, "profiles", "r04_pmc"), "--no-copy", "--out", str(out),
+                    os.path.join(ROOT, "profiles", "r05_pmc"), "--no-copy", "--out", str(out),
                     "--build-id", _build.source_hash()], check=True, capture_output=True)
     got = json.loads(out.read_text())["entries"]
     with open(bench.PMC_SUMMARY) as f:
