@@ -89,6 +89,7 @@ def trajectory(env_id, N, force_valu=False, over=None, kernel=None):
                           traj_ge=os.environ.get("FGX_TRAJ_GE"), traj_rc=os.environ.get("FGX_TRAJ_RC"),
                           traj_nt=os.environ.get("FGX_TRAJ_NT"), traj_sep=os.environ.get("FGX_TRAJ_SEP"),
                           traj_align=os.environ.get("FGX_TRAJ_ALIGN"), traj_threads=os.environ.get("FGX_TRAJ_THREADS"),
+                          traj_pipe=os.environ.get("FGX_TRAJ_PIPE"),
                           kernel_us=t * 1e6, GBps=bytes_ / t / 1e9, hbm_frac=bytes_ / t / 8e12,
                           mfma_TFLOPs=flops / t / 1e12, mfma_frac_f32=flops / t / 157.3e12)), flush=True)
 
@@ -363,10 +364,9 @@ if __name__ == "__main__":
         traj_run_scan()
     if "dmp" in which:   # DMP trajectory: the default shape against explicit ones
         for kv in ({}, {"FGX_TRAJ_GE": "6"}, {"FGX_TRAJ_GE": "8"}, {"FGX_TRAJ_GE": "10"},
-                   {"FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "6", "FGX_TRAJ_RC": "64"}, {"FGX_TRAJ_GE": "4"},
-                   {"FGX_TRAJ_GE": "8", "FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "6", "FGX_TRAJ_NT": "0"},
-                   {"FGX_TRAJ_THREADS": "128", "FGX_TRAJ_GE": "6"}, {}):
-            for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN", "FGX_TRAJ_THREADS"):
+                   {"FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "8", "FGX_TRAJ_RC": "32"}, {}):
+            for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT", "FGX_TRAJ_SEP", "FGX_TRAJ_ALIGN", "FGX_TRAJ_THREADS",
+                      "FGX_TRAJ_PIPE"):
                 os.environ.pop(k, None)
             os.environ.update(kv)
             trajectory("fancy_DMP/LongSimpleReacher-v0", 65536)
