@@ -30,6 +30,10 @@ CASES = [
                                                             "condition_on_desired": True}}, {}, 511, 2),
     ("fancy_ProMP/LongSimpleReacher-v0", {"basis_generator_kwargs": {"num_basis": 7}}, {}, 300, 0),
     ("fancy_DMP/HoleReacher-v0", None, {"n_links": 3}, 129, 0),        # the n_links instantiations
+    # T * dof not a multiple of 4: pieces stored as dwords (T = 201 / 199, 2 links)
+    ("fancy_ProMP/SimpleReacher-v0", {"black_box_kwargs": {"duration": 2.01, "replanning_schedule": fgx.ReplanEvery(201)}},
+     {}, 300, 0),
+    ("fancy_DMP/SimpleReacher-v0", {"black_box_kwargs": {"duration": 1.99}}, {}, 97, 0),
 ]
 
 
