@@ -31,8 +31,8 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
 
 // the helper form (fgx_jl.h, HLP 1 / 2): ProMP on the column table; FGX_JL_HELPER=0 / 1 / 2 forces
 inline int jl_helper(const fgx::DevCfg& c) {
-  if (c.T > 256) return 0;   // (HLP 2 stages at most 272 column rows)
   if (const char* v = std::getenv("FGX_JL_HELPER")) return v[0] == '1' ? 1 : v[0] == '2' ? 2 : 0;
+  (void)c;
   return 0;
 }
 

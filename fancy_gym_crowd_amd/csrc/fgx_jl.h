@@ -36,9 +36,8 @@ namespace fgx {
 typedef float jl_f4 __attribute__((ext_vector_type(4)));
 
 // HLP: one joint wave and one helper wave per workgroup (k_episode_jl's helper form, below);
-// 1: the helper produces chunk ch + 1 while the joint wave runs chunk ch (two buffers); 2: pipelined —
-// the helper runs two chunks ahead from the basis columns staged in LDS (three buffers) and the joint
-// wave reads the next chunk before running the current one
+// 1: the helper hands over f32 trajectory chunks and the joint wave writes a^2, 2: f64 chunks (the
+// conversions on the helper) and the joint wave writes a (the squares on the helper)
 template <int NL, int HLP = 0>
 struct JlShape {
   static constexpr int G = 64 / NL;             // envs per wave
@@ -62,15 +61,12 @@ struct JlShape {
   // HLP: after the exchange rows, the helper's two trajectory chunk buffers ([buf][PVQ][lane] 16-B
   // quads: HLP 1 P[0..3], P[4..7], V[0..3], V[4..7] as f32; HLP 2 P[0..1] .. V[6..7] as f64) and its
   // hand-over record (the pairwise slots, the look-ahead)
-  static constexpr int PVQ = 4;
-  static constexpr int NPV = HLP == 2 ? 3 : 2;   // trajectory chunk buffers
-  static constexpr int LRT = 256 + 16;           // HLP 2: staged column rows (T <= 256)
+  static constexpr int PVQ = HLP == 2 ? 8 : 4;
   static constexpr size_t ex_bytes() { return ((size_t)WAVES * 16 * XS * sizeof(double) + 15) & ~(size_t)15; }
-  static constexpr size_t pv_bytes() { return HLP ? (size_t)NPV * PVQ * 64 * 16 : 0; }
+  static constexpr size_t pv_bytes() { return HLP ? (size_t)2 * PVQ * 64 * 16 : 0; }
   static constexpr size_t ho_bytes() { return HLP ? (size_t)64 * (2 * SPW + 1) * sizeof(double) : 0; }
-  static constexpr size_t col_bytes(int ncols) { return HLP == 2 ? (size_t)ncols * LRT * sizeof(float) : 0; }
-  static constexpr size_t lds_bytes(int ncols = 7) {
-    const size_t ex = ex_bytes() + pv_bytes() + ho_bytes() + col_bytes(ncols);
+  static constexpr size_t lds_bytes() {
+    const size_t ex = ex_bytes() + pv_bytes() + ho_bytes();
     const size_t ga = (size_t)GF * EPB * sizeof(double);
     return ex > ga ? ex : ga;
   }
@@ -436,38 +432,53 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  auto pv_put = [&](int buf, const float* Pv, const float* Vv) __attribute__((always_inline)) {
-    jl_f4* b = pvb + buf * (S::PVQ * 64) + lane;
-    b[0] = (jl_f4){Pv[0], Pv[1], Pv[2], Pv[3]};
-    b[64] = (jl_f4){Pv[4], Pv[5], Pv[6], Pv[7]};
-    b[128] = (jl_f4){Vv[0], Vv[1], Vv[2], Vv[3]};
-    b[192] = (jl_f4){Vv[4], Vv[5], Vv[6], Vv[7]};
-  };
-  auto pv_get = [&](int buf, float* Pv, float* Vv) __attribute__((always_inline)) {
-    const jl_f4* b = pvb + buf * (S::PVQ * 64) + lane;
-    const jl_f4 p0 = b[0], p1 = b[64], v0 = b[128], v1 = b[192];
+  typedef double jl_d2 __attribute__((ext_vector_type(2)));
+  auto pv_put = [&](int ch, const float* Pv, const float* Vv) __attribute__((always_inline)) {
+    jl_f4* b = pvb + (ch & 1) * (S::PVQ * 64) + lane;
+    if constexpr (HLP == 2) {
+      jl_d2* bd = (jl_d2*)b;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { Pv[j] = p0[j]; Pv[4 + j] = p1[j]; Vv[j] = v0[j]; Vv[4 + j] = v1[j]; }
+      for (int i = 0; i < 4; ++i) {
+        bd[i * 64] = (jl_d2){(double)Pv[2 * i], (double)Pv[2 * i + 1]};
+        bd[(4 + i) * 64] = (jl_d2){(double)Vv[2 * i], (double)Vv[2 * i + 1]};
+      }
+    } else {
+      b[0] = (jl_f4){Pv[0], Pv[1], Pv[2], Pv[3]};
+      b[64] = (jl_f4){Pv[4], Pv[5], Pv[6], Pv[7]};
+      b[128] = (jl_f4){Vv[0], Vv[1], Vv[2], Vv[3]};
+      b[192] = (jl_f4){Vv[4], Vv[5], Vv[6], Vv[7]};
+    }
   };
-  // HLP 2: the column table's rows [s0u, s0u + LRT) of the NBL basis columns and the dt / 1/dt columns
-  // in LDS (column j at lcol + j * LRT; a chunk starting at sample k0 reads its 8 rows at k0 + 8, 16-B
-  // aligned), so the helper's chunk reads are LDS reads it can issue early
-  float* lcol = (float*)((char*)lds_jl + S::ex_bytes() + S::pv_bytes() + S::ho_bytes());
-  auto traj_load_lds = [&](int k0, Cols& cl) __attribute__((always_inline)) {
-    auto ld8 = [&](int col) __attribute__((always_inline)) {
-      const jl_f4* q4 = (const jl_f4*)(lcol + col * S::LRT + k0 + 8);
-      const jl_f4 a = q4[0], b = q4[1];
-      return (f8u){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    };
+  auto pv_get = [&](int ch, float* Pv, float* Vv) __attribute__((always_inline)) {
+    const jl_f4* b = pvb + (ch & 1) * (S::PVQ * 64) + lane;
+    if constexpr (HLP == 2) {
+      const jl_d2* bd = (const jl_d2*)b;
 #pragma unroll
-    for (int j = 0; j < NBL; ++j) cl.b[j] = ld8(j);
-    cl.dt = ld8(NBL);
-    cl.rd = ld8(NBL + 1);
+      for (int i = 0; i < 4; ++i) {
+        const jl_d2 p = bd[i * 64], v = bd[(4 + i) * 64];
+        Pv[2 * i] = (float)p[0]; Pv[2 * i + 1] = (float)p[1];
+        Vv[2 * i] = (float)v[0]; Vv[2 * i + 1] = (float)v[1];
+      }
+    } else {
+      const jl_f4 p0 = b[0], p1 = b[64], v0 = b[128], v1 = b[192];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { Pv[j] = p0[j]; Pv[4 + j] = p1[j]; Vv[j] = v0[j]; Vv[4 + j] = v1[j]; }
+    }
+  };
+  auto pv_get_d = [&](int ch, double* Pd, double* Vd) __attribute__((always_inline)) {   // HLP 2
+    const jl_d2* bd = (const jl_d2*)(pvb + (ch & 1) * (S::PVQ * 64) + lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const jl_d2 p = bd[i * 64], v = bd[(4 + i) * 64];
+      Pd[2 * i] = p[0]; Pd[2 * i + 1] = p[1];
+      Vd[2 * i] = v[0]; Vd[2 * i + 1] = v[1];
+    }
   };
   // the helper: chunk 0's trajectory (Traj::at through the scalar rows, as run()), then per chunk ch
   // the trajectory of chunk ch + 1 (with the plan-end patch of fast_iter) and the reduction of chunk
   // ch - 1 in fast_range's phases; after the last chunk the hand-over record
   auto helper_fast = [&](int nf, int na) __attribute__((always_inline)) {
+    traj(0, P, V, std::false_type{}, std::true_type{});
     float vl = 0.0f;   // fast_iter's vlast: the last (patched) velocity of the previous chunk
     auto patch = [&](int m, float* Vv) __attribute__((always_inline)) {
       if (__builtin_expect(m == cpch, 0)) {
@@ -480,107 +491,73 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
         }
       }
     };
-    auto handover = [&]() __attribute__((always_inline)) {
+    patch(0, V);
+    vl = V[7];
+    pv_put(0, P, V);
+    hl_barrier();
+    for (int ch = 0; ch < nf; ++ch) {
+      const int k0 = ch * 8;
+      Cols cl;
+      traj_load(k0 + 8, cl);
+      double rv[SPW][NL];
+      if (ch >= 1) reduce_load(ch - 1, rv);
+      __builtin_amdgcn_sched_barrier(0);
+      traj_fast(k0 + 8, cl, Pn, Vn);
+      patch(ch + 1, Vn);
+      if constexpr (HLP == 2) {   // the joint wave wrote a: the squares here
 #pragma unroll
-      for (int sl = 0; sl < SPW; ++sl) { hob[sl * 64 + lane] = A[sl]; hob[(SPW + sl) * 64 + lane] = B[sl]; }
-      hob[2 * SPW * 64 + lane] = __builtin_bit_cast(double, (f32x2){tg.cur[0], tg.vprev[0]});
-    };
-    if constexpr (HLP == 2) {
-      {   // the columns to LDS (every row a chunk can read: k0 + 8 + 7 <= T + 15)
-        const int RT = tables_t_rows(c.rows);
-        const float* tt = s.tables_t;
-        const int lr = min(S::LRT, (c.T + 16 + 7) & ~7);
-        for (int i = lane; i < (NBL + 2) * lr; i += 64) {
-          const int col = i / lr, r = i - col * lr;
-          lcol[col * S::LRT + r] = tt[(size_t)col * RT + s0u + r];
-        }
-        wave_lds_sync();
+        for (int sl = 0; sl < SPW; ++sl)
+#pragma unroll
+          for (int dd = 0; dd < NL; ++dd) rv[sl][dd] = rv[sl][dd] * rv[sl][dd];
       }
-      traj(0, P, V, std::false_type{}, std::true_type{});
-      patch(0, V);
-      vl = V[7];
-      pv_put(0, P, V);
-      {   // chunk 1
-        Cols cl;
-        traj_load_lds(8, cl);
-        traj_fast(8, cl, Pn, Vn);
-        patch(1, Vn);
-        vl = Vn[7];
-        pv_put(1, Pn, Vn);
+      vl = Vn[7];
+      pv_put(ch + 1, Pn, Vn);
+      if (ch >= 1) {
+        if (ch < na) reduce_fast(rv, std::integral_constant<int, 1>{});
+        else reduce_fast(rv, std::integral_constant<int, 2>{});
+      }
+      if (ch == nf - 1) {
+#pragma unroll
+        for (int sl = 0; sl < SPW; ++sl) { hob[sl * 64 + lane] = A[sl]; hob[(SPW + sl) * 64 + lane] = B[sl]; }
+        hob[2 * SPW * 64 + lane] = __builtin_bit_cast(double, (f32x2){tg.cur[0], tg.vprev[0]});
       }
       hl_barrier();
-      for (int ch = 0; ch < nf; ++ch) {
-        const int m = ch + 2;   // the chunk produced in this phase (<= nf: the slow chunks' first)
-        Cols cl;
-        if (m <= nf) traj_load_lds(8 * m, cl);
-        double rv[SPW][NL];
-        if (ch >= 1) reduce_load(ch - 1, rv);
-        if (m <= nf) {
-          traj_fast(8 * m, cl, Pn, Vn);
-          patch(m, Vn);
-          vl = Vn[7];
-          pv_put(m % 3, Pn, Vn);
-        }
-        if (ch >= 1) {
-          if (ch < na) reduce_fast(rv, std::integral_constant<int, 1>{});
-          else reduce_fast(rv, std::integral_constant<int, 2>{});
-        }
-        if (ch == nf - 1) handover();
-        hl_barrier();
-      }
-    } else {
-      traj(0, P, V, std::false_type{}, std::true_type{});
-      patch(0, V);
-      vl = V[7];
-      pv_put(0, P, V);
-      hl_barrier();
-      for (int ch = 0; ch < nf; ++ch) {
-        const int k0 = ch * 8;
-        Cols cl;
-        traj_load(k0 + 8, cl);
-        double rv[SPW][NL];
-        if (ch >= 1) reduce_load(ch - 1, rv);
-        __builtin_amdgcn_sched_barrier(0);
-        traj_fast(k0 + 8, cl, Pn, Vn);
-        patch(ch + 1, Vn);
-        vl = Vn[7];
-        pv_put((ch + 1) & 1, Pn, Vn);
-        if (ch >= 1) {
-          if (ch < na) reduce_fast(rv, std::integral_constant<int, 1>{});
-          else reduce_fast(rv, std::integral_constant<int, 2>{});
-        }
-        if (ch == nf - 1) handover();
-        hl_barrier();
-      }
     }
   };
   // the joint wave: per chunk the f64 chain on the helper's trajectory; then chunk nf's trajectory
   // (the slow chunks' first) and the hand-over
   auto joint_fast = [&](int nf) __attribute__((always_inline)) {
-    hl_barrier();   // the first chunks' trajectory
-    if constexpr (HLP == 2) {
-      pv_get(0, P, V);
-      for (int ch = 0; ch < nf; ++ch) {
-        pv_get((ch + 1) % 3, Pn, Vn);   // the next chunk, read ahead of this chunk's chain
-        dyn(ch * 8, P, V, sq, std::true_type{}, std::integral_constant<int, 2>{});   // ProMP: NaN-free
-        plast = P[7];
-        vlast = V[7];
-        write_sq(ch, sq);
-        hl_barrier();
+    hl_barrier();   // chunk 0's trajectory
+    for (int ch = 0; ch < nf; ++ch) {
+      if constexpr (HLP == 2) {
+        // dyn's fast, NaN-free form on the helper's f64 chunk, writing a (the last fast chunk a^2:
+        // the slow chunks reduce it here)
+        double Pd[8], Vd[8];
+        pv_get_d(ch, Pd, Vd);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { P[j] = Pn[j]; V[j] = Vn[j]; }
-      }
-    } else {
-      for (int ch = 0; ch < nf; ++ch) {
-        pv_get(ch & 1, P, V);
+        for (int j = 0; j < 8; ++j) {
+          const double u = fadd(pg * fsub(Pd[j], q), dg * fsub(Vd[j], qd));
+          const double a = __builtin_fmin(__builtin_fmax(u, act_lo), act_hi);
+          qd = fadd(qd, dt * a);
+          q = fadd(q, dt * qd);
+          sq[j] = a;
+        }
+        if (ch == nf - 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sq[j] = sq[j] * sq[j];
+        }
+        plast = (float)Pd[7];
+        vlast = (float)Vd[7];
+      } else {
+        pv_get(ch, P, V);
         dyn(ch * 8, P, V, sq, std::true_type{}, std::integral_constant<int, 2>{});   // ProMP: NaN-free
         plast = P[7];
         vlast = V[7];
-        write_sq(ch, sq);
-        hl_barrier();
       }
-      pv_get(nf & 1, P, V);
+      write_sq(ch, sq);
+      hl_barrier();
     }
+    pv_get(nf, P, V);
 #pragma unroll
     for (int sl = 0; sl < SPW; ++sl) { A[sl] = hob[sl * 64 + lane]; B[sl] = hob[(SPW + sl) * 64 + lane]; }
     const f32x2 cv = __builtin_bit_cast(f32x2, hob[2 * SPW * 64 + lane]);
