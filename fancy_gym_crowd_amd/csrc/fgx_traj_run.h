@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
   const int T = c.T;
   const int str = TrajT::KS ? TrajT::KS : c.stride;
   float* tab = (float*)lds_run;
-  const int tab_f = c.rows * c.stride;
+  // (DMP reads its rows from global memory: by scalar loads when the wave's plans start on one row)
+  const int tab_f = SEQ ? 0 : c.rows * c.stride;
   const int nthr = blockDim.x;   // 64 .. kTrajRunThreads (host: DMP one wave, else 256)
   for (int i = t; i < tab_f; i += nthr) tab[i] = s.tables[i];
   // LDS floats per env and region (16-B aligned): a 32-float carry area (the tail of the previous
@@ -152,14 +153,26 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
     for (int row0 = 0; row0 < T; row0 += RC) {
       const int rows = min(RC, T - row0);
       if constexpr (SEQ) {
+        const uint64_t am = __ballot(act);
+        const int s0l = __builtin_amdgcn_readlane(s0, am ? __builtin_ctzll(am) : 0);
+        const bool uni = __ballot(act && s0 != s0l) == 0;
         if (act) {
           float pos[1], vel[1];
           float* dp = rpos + je * ESR + CA + dl;
           float* dv = rvel + je * ESR + CA + dl;
-          for (int k = row0; k < row0 + rows; ++k) {
-            tg.template at_rows<false>(c, k, tab + (size_t)(s0 + k + 1) * str, pos, vel);
-            dp[(k - row0) * NL] = pos[0];
-            dv[(k - row0) * NL] = vel[0];
+          if (uni) {   // rows by scalar loads
+            const cfloat_ptr sb = (cfloat_ptr)(uintptr_t)s.tables + (size_t)(s0l + 1) * str;
+            for (int k = row0; k < row0 + rows; ++k) {
+              tg.template at_rows<false>(c, k, sb + (size_t)k * str, pos, vel);
+              dp[(k - row0) * NL] = pos[0];
+              dv[(k - row0) * NL] = vel[0];
+            }
+          } else {     // (plans starting on different rows: per-lane loads)
+            for (int k = row0; k < row0 + rows; ++k) {
+              tg.template at_rows<false>(c, k, s.tables + (size_t)(s0 + k + 1) * str, pos, vel);
+              dp[(k - row0) * NL] = pos[0];
+              dv[(k - row0) * NL] = vel[0];
+            }
           }
         }
         lds_barrier();
@@ -239,7 +252,9 @@ __global__ __launch_bounds__(kTrajRunThreads) void k_traj_run(DevCfg c, DevState
 //     stores: 162-167 us (regular stores 167-190; 12 x 32 / 64 rows: 165-205; 17 / 25 envs: 175-218;
 //     pieces ending on 128-B lines or on rows: within the sessions' noise, r05_s12_traj_sweep.jsonl).
 //     DMP is sensitive to the workgroups per CU (LDS-bound; its joint lanes fill wave 0, every wave
-//     stores): four per CU 272 us, five 169-183 us, one-wave workgroups 480 us (r05_s15..s17_dmp_shapes).
+//     stores): four per CU 272 us, five 169-183 us, one-wave workgroups 480 us (r05_s15..s17_dmp_shapes);
+//     its rows by scalar loads instead of an LDS table copy per workgroup: six per CU, 154-165 us
+//     (r05_s22_dmp_scalar_rows.jsonl).
 // FGX_TRAJ_GE / _RC / _NT=0|1 / _SEP=0|1 / _ALIGN=0 / _THREADS / _PERCU override (A/B).
 struct TrajRunShape {
   int GE, RC, nt, sep, threads, per_cu;
@@ -247,7 +262,8 @@ struct TrajRunShape {
 };
 // sep: positions, then velocities through one region (ProMP / ProDMP)
 inline size_t traj_run_lds(const DevCfg& c, int GE, int RC, int sep = 0) {
-  return (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4 + (sep ? 1 : 2) * (size_t)GE * (32 + (size_t)RC * c.nl) * 4 +
+  return (c.mp == MP_DMP ? 0 : (((size_t)c.rows * c.stride + 3) & ~(size_t)3) * 4) +
+         (sep ? 1 : 2) * (size_t)GE * (32 + (size_t)RC * c.nl) * 4 +
          2 * (size_t)GE * 32 * 4;
 }
 inline TrajRunShape traj_run_shape(const DevCfg& c) {
