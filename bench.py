@@ -9,8 +9,9 @@ carries a weak-scaling measurement (65536 envs per GPU) as a secondary field.
 For N > 1, `bench.py --gpus N` starts the N ranks itself (torch.distributed.run as a child process,
 one process per GPU) unless a launcher already did (WORLD_SIZE set; it must equal --gpus); with
 fewer visible GPUs than ranks they share cuda:0 over gloo (rehearsal).  Env shards are independent
-(seeds = global env index, the rank's rows of the global parameter matrix), RCCL only gathers the
-final episode returns.  Prints ONE JSON line on rank 0.
+(seeds = global env index, the rank's rows of the global parameter matrix); the only exchange is an
+RCCL all_gather of the episode returns after EVERY BB step (one episode each), captured with the
+episode launches in one HIP graph and inside the timed window.  Prints ONE JSON line on rank 0.
 
 A "step" = one BlackBoxWrapper.step for every env (black_box_wrapper.py:170-253): MP trajectory
 (200 samples), PD control, 200 reacher substeps, return, VectorEnv auto-reset.
@@ -267,76 +268,102 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     tr = torch.empty(N, dtype=torch.uint8, device=dev)
     tl = torch.empty(N, dtype=torch.int32, device=dev)
     acc = env.new_inner_steps()   # device counter of inner env steps
+    # every BB step ends with the episode-return all_gather over RCCL/xGMI (the path's only
+    # exchange): one all_gather_into_tensor of this rank's [N] f64 returns
+    gbuf = torch.empty(N * world, dtype=torch.float64, device=coll_dev) if dist is not None else None
+    n_gathers = [0]
+
+    def bb_step(count=True):
+        env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc if count else None)
+        if gbuf is not None:
+            shard.gather_returns_into(gbuf, ret)
+            n_gathers[0] += 1
 
     for _ in range(W):
-        env.step_into(params, obs, ret, te, tr, tl, fobs)
+        bb_step(count=False)
     torch.cuda.synchronize()
-    graph = None
-    if use_graph:
-        # the K BB-step launches captured once in a HIP graph (the same kernels on the same state;
-        # removes the per-launch host round trip between dependent steps)
+
+    def capture(fn):
         try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
                 for _ in range(K):
-                    env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
+                    fn()
             torch.cuda.synchronize()
-        except Exception as e:   # capture unsupported: time the eager launches instead
-            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
-            graph = None
+            return g, None
+        except Exception as e:   # capture unsupported: eager launches instead
+            torch.cuda.synchronize()
+            return None, str(e)
+
+    # kernel-only time: the K episode launches alone in a HIP graph, HIP events on the launch stream
+    # (outside the timed region; it separates kernel time from the per-step collective)
+    kgraph = kerr = None
+    if use_graph:
+        kgraph, kerr = capture(lambda: env.step_into(params, obs, ret, te, tr, tl, fobs))
+    ek0, ek1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ek0.record()
+    if kgraph is not None:
+        kgraph.replay()
+    else:
+        for _ in range(K):
+            env.step_into(params, obs, ret, te, tr, tl, fobs)
+    ek1.record()
+    torch.cuda.synchronize()
+    kern_ms = ek0.elapsed_time(ek1) / K
+    del kgraph
+
+    # the timed BB steps: K x (episode launch [+ return all_gather]).  RCCL collectives on device
+    # buffers are captured into the same HIP graph as the kernels; the gloo rehearsal (host
+    # buffers) cannot be captured and runs eagerly.
+    graph, gerr = None, None
+    if use_graph and (gbuf is None or gbuf.is_cuda):
+        graph, gerr = capture(lambda: bb_step())
+        if gerr:
+            print(f"[bench] graph capture failed ({gerr}); timing eager launches", file=sys.stderr)
+    n_captured = n_gathers[0] - W
+    n_gathers[0] = 0
     acc.zero_()
-    # HIP events on the stream the kernels are launched on (the current stream of step_into)
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     if graph is not None:
-        ev0[0].record()
         graph.replay()
-        ev1[0].record()
+        n_gathers[0] = n_captured
     else:
-        for k in range(K):
-            ev0[k].record()
-            env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc)
-            ev1[k].record()
-    # the collective and the closing barrier are timed apart from the kernels (per rank), so that a
-    # multi-GPU point separates kernel time from collective latency
-    coll_ms = barrier_ms = 0.0
-    if dist is not None:   # final episode-return gather over RCCL/xGMI (the path's only exchange)
-        ec0, ec1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ec0.record()
-        all_ret = shard.gather_returns(ret.to(coll_dev))
-        ec1.record()
+        for _ in range(K):
+            bb_step()
+    ev1.record()
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0          # closing barrier below is outside this window
+    step_ms = ev0.elapsed_time(ev1) / K
+    barrier_ms = 0.0
     if dist is not None:
         tb = time.perf_counter()
         dist.barrier()
         barrier_ms = (time.perf_counter() - tb) * 1e3
-        coll_ms = ec0.elapsed_time(ec1)
-    elapsed = time.perf_counter() - t0
     inner_local = int(acc.sum().item())
-    if graph is not None:
-        kern_ms = ev0[0].elapsed_time(ev1[0]) / K
-    else:
-        kern_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
-    timing_local = [kern_ms, coll_ms, barrier_ms, elapsed * 1e3]
+    coll_ms = max(0.0, step_ms - kern_ms) if dist is not None else 0.0
+    timing_local = [kern_ms, step_ms, coll_ms, barrier_ms, elapsed * 1e3, float(n_gathers[0])]
     if dist is not None:
         elapsed = shard.max_over_ranks(elapsed, coll_dev)
         inner = shard.sum_over_ranks(inner_local, coll_dev)
-        assert all_ret.numel() == N * world
         shards = shard.gather_ints([lo, lo + N, inner_local], coll_dev)
         timing = shard.gather_floats(timing_local, coll_dev)
     else:
         inner = inner_local
         shards = [[lo, lo + N, inner_local]]
         timing = [timing_local]
-    per_rank = [{"rank": i, "kernel_ms_per_step": t[0], "collective_ms": t[1], "barrier_ms": t[2], "wall_ms": t[3]}
-                for i, t in enumerate(timing)]
+    per_rank = [{"rank": i, "kernel_ms_per_step": t[0], "step_ms": t[1], "collective_ms_per_step": t[2],
+                 "barrier_ms": t[3], "wall_ms": t[4], "gathers": int(t[5])} for i, t in enumerate(timing)]
+    launch = "hip graph of the K steps" if graph is not None else "eager"
+    if gbuf is not None:
+        launch += (" (episode kernel + RCCL all_gather of the returns per BB step, captured)" if graph is not None
+                   else " (episode kernel + return all_gather per BB step)")
     return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
-                shards=shards, per_rank=per_rank,
-                launch="hip graph of the K steps" if graph is not None else "eager")
+                shards=shards, per_rank=per_rank, launch=launch, gathers=n_gathers[0], capture_error=gerr)
 
 
 def roofline(env_id, env, N, kern_ms, inner_local, K, simds, build_id):
@@ -436,6 +463,14 @@ def main():
     coll_dev = "cpu" if rehearsal else torch.device("cuda", gpu)
     if world > 1 or args.force_dist:
         import torch.distributed as dist
+        if not launched:   # --force-dist without a launcher: a one-rank group on this host
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                free_port = sk.getsockname()[1]
+            for k, v in (("WORLD_SIZE", "1"), ("RANK", "0"), ("LOCAL_RANK", "0"),
+                         ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(free_port))):
+                os.environ.setdefault(k, v)
         torch.cuda.set_device(gpu)
         if rehearsal:
             dist.init_process_group("gloo")
@@ -480,7 +515,7 @@ def main():
                     "default_rng(1234).standard_normal((N_global, 25), f32)",
             "config": {"workload": args.env_id, "global_envs": n_local * world, "envs_per_gpu": n_local,
                        "T": env.T, "launch": r["launch"],
-                       "parallelism": f"env-shard x{world} (RCCL all_gather of returns only)"
+                       "parallelism": f"env-shard x{world} (RCCL all_gather of the returns after every BB step)"
                        + (" [rehearsal: ranks share cuda:0, gloo]" if rehearsal else "")},
             "ranks_seen": dist.get_world_size() if dist is not None else 1,
             "backend": dist.get_backend() if dist is not None else None,
@@ -488,14 +523,20 @@ def main():
                                                      else "")) if launched else "single process",
             # per rank: [first global env, end, inner env steps in the timed region]
             "shards": r["shards"],
-            # per rank: kernel time per BB step (HIP events), the return all_gather (events around it)
-            # and the closing barrier (host), all inside the timed region
+            # per rank: kernel time per BB step (HIP events around a kernel-only graph of K steps),
+            # the timed BB step (episode + return all_gather, HIP events), their difference = the
+            # per-step collective, the closing barrier (host, outside the value window) and the
+            # number of return gathers inside the timed region (= steps when N > 1)
             "timing": {"kernel_ms_per_step_max": max(t["kernel_ms_per_step"] for t in r["per_rank"]),
-                       "collective_ms_max": max(t["collective_ms"] for t in r["per_rank"]),
+                       "step_ms_max": max(t["step_ms"] for t in r["per_rank"]),
+                       "collective_ms_per_step_max": max(t["collective_ms_per_step"] for t in r["per_rank"]),
                        "barrier_ms_max": max(t["barrier_ms"] for t in r["per_rank"]),
+                       "gathers": r["gathers"],
                        "per_rank": r["per_rank"]},
             "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds, lib_build_id()),
         }
+        if r["capture_error"]:
+            line["timing"]["capture_error"] = r["capture_error"]
         if weak is not None:
             line["weak_scaling"] = weak
         if world == 1 and env.T % 4 == 0:

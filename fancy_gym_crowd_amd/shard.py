@@ -35,6 +35,19 @@ def gather_returns(ret, group=None):
     return torch.cat(parts)
 
 
+def gather_returns_into(out, ret, group=None):
+    """all_gather this rank's returns [n] into the preallocated `out` [world * n] (global env order)
+    with one all_gather_into_tensor.  On a device `out` (RCCL) this is a single collective on the
+    current stream, so it can be captured in a HIP graph after each BB step; a host `out` (gloo
+    rehearsal) takes a host copy of `ret` first."""
+    import torch.distributed as dist
+    if out.numel() != ret.numel() * dist.get_world_size(group):
+        raise ValueError("gather buffer must hold world_size x the local returns")
+    src = ret if out.device == ret.device else ret.to(out.device)
+    dist.all_gather_into_tensor(out, src.contiguous(), group=group)
+    return out
+
+
 def max_over_ranks(x, device, group=None):
     """Wall time of the job = max over ranks."""
     import torch.distributed as dist

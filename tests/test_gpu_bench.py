@@ -58,6 +58,9 @@ def test_bench_gpus2_spawns_two_ranks():
     assert sum(s[2] for s in d["shards"]) == 65536 * 200 * 2
     assert d["value"] == pytest.approx(65536 * 200 / (d["ms_per_step"] * 1e-3), rel=1e-6)
     _check_roofline(d["roofline"])
+    # the return all_gather runs after every timed BB step on every rank
+    assert d["timing"]["gathers"] == 2
+    assert [p["gathers"] for p in d["timing"]["per_rank"]] == [2, 2]
 
 
 def test_bench_gpus_mismatch_is_refused():

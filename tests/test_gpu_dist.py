@@ -100,3 +100,4 @@ def test_bench_distributed_leg_two_ranks():
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert d["config"]["global_envs"] == 2048 and d["config"]["envs_per_gpu"] == 1024
     assert d["value"] > 0 and d["steps"] == 3
+    assert d["timing"]["gathers"] == 3 and all(p["gathers"] == 3 for p in d["timing"]["per_rank"])

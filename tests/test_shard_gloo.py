@@ -29,6 +29,15 @@ def _worker(rank, world, port, q):
     # a stand-in "return" that depends on the global env index and the env's parameter row
     ret = torch.from_numpy(mine.sum(1).astype(np.float64)) + torch.arange(lo, hi, dtype=torch.float64)
     all_ret = shard.gather_returns(ret)
+    # bench.py's per-BB-step form: one all_gather_into_tensor into a preallocated buffer
+    buf = torch.empty(n * world, dtype=torch.float64)
+    assert shard.gather_returns_into(buf, ret) is buf
+    assert torch.equal(buf, all_ret)
+    try:
+        shard.gather_returns_into(torch.empty(n, dtype=torch.float64), ret)
+        raise AssertionError("short gather buffer accepted")
+    except ValueError:
+        pass
     t = shard.max_over_ranks(1.0 + rank, "cpu")
     s = shard.sum_over_ranks(200 * n, "cpu")
     q.put((rank, lo, hi, all_ret.numpy(), t, s))
