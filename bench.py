@@ -245,7 +245,7 @@ def _cpu_worker(args):
 
 
 # ----------------------------------------------------------------------------- GPU run
-def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev):
+def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev, overlap=True):
     """K timed BB steps of this rank's shard (global envs [rank * n_local, (rank + 1) * n_local)),
     bracketed by barrier + synchronize on both sides.  Returns wall time (max over ranks), inner
     steps (sum over ranks), this rank's event time per step, inner steps and the env."""
@@ -269,19 +269,51 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     tl = torch.empty(N, dtype=torch.int32, device=dev)
     acc = env.new_inner_steps()   # device counter of inner env steps
     # every BB step ends with the episode-return all_gather over RCCL/xGMI (the path's only
-    # exchange): one all_gather_into_tensor of this rank's [N] f64 returns
+    # exchange): one all_gather_into_tensor of this rank's [N] f64 returns.
+    # On device buffers (RCCL) the returns are double-buffered and the gather of step k runs on a
+    # side stream while the episode kernel of step k + 1 runs (it reads nothing the gather
+    # writes); step k + 2 waits for gather k before it overwrites that return buffer.  The gloo
+    # rehearsal (host buffers) gathers in line.
     gbuf = torch.empty(N * world, dtype=torch.float64, device=coll_dev) if dist is not None else None
-    n_gathers = [0]
+    overlap = overlap and gbuf is not None and gbuf.is_cuda
+    rets = [ret, torch.empty_like(ret)] if overlap else [ret, ret]
+    gbufs = [gbuf, torch.empty_like(gbuf)] if overlap else [gbuf, gbuf]
+    comm = torch.cuda.Stream(device=dev) if overlap else None
+    st = {"k": 0, "gathers": 0, "free": [None, None], "pending": False}
 
     def bb_step(count=True):
-        env.step_into(params, obs, ret, te, tr, tl, fobs, inner_steps=acc if count else None)
-        if gbuf is not None:
-            shard.gather_returns_into(gbuf, ret)
-            n_gathers[0] += 1
+        s = st["k"] % 2
+        st["k"] += 1
+        if overlap and st["free"][s] is not None:
+            torch.cuda.current_stream().wait_event(st["free"][s])
+        env.step_into(params, obs, rets[s], te, tr, tl, fobs, inner_steps=acc if count else None)
+        if gbuf is None:
+            return
+        st["gathers"] += 1
+        if not overlap:
+            shard.gather_returns_into(gbufs[s], rets[s])
+            return
+        ready = torch.cuda.Event()
+        ready.record()
+        comm.wait_event(ready)
+        with torch.cuda.stream(comm):
+            shard.gather_returns_into(gbufs[s], rets[s])
+            done = torch.cuda.Event()
+            done.record()
+        st["free"][s] = done
+        st["pending"] = True
+
+    def join():
+        """the launch stream waits for the gathers still in flight on the side stream"""
+        if st["pending"]:
+            torch.cuda.current_stream().wait_stream(comm)
+        st["free"], st["pending"] = [None, None], False
 
     for _ in range(W):
         bb_step(count=False)
+    join()
     torch.cuda.synchronize()
+    st["gathers"] = 0
 
     def capture(fn):
         try:
@@ -289,27 +321,39 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
             with torch.cuda.graph(g):
                 for _ in range(K):
                     fn()
+                join()
             torch.cuda.synchronize()
             return g, None
         except Exception as e:   # capture unsupported: eager launches instead
             torch.cuda.synchronize()
             return None, str(e)
 
+    def timed_graph(g, fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if g is not None:
+            g.replay()
+        else:
+            for _ in range(K):
+                fn()
+            join()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / K
+
+    # the return gather alone (K captured all_gathers): the collective's own cost per BB step
+    gather_ms = None
+    if gbuf is not None and gbuf.is_cuda and use_graph:
+        cg, _ = capture(lambda: shard.gather_returns_into(gbuf, ret))
+        if cg is not None:
+            gather_ms = timed_graph(cg, None)
+            del cg
+
     # kernel-only time: the K episode launches alone in a HIP graph, HIP events on the launch stream
     # (outside the timed region; it separates kernel time from the per-step collective)
-    kgraph = kerr = None
-    if use_graph:
-        kgraph, kerr = capture(lambda: env.step_into(params, obs, ret, te, tr, tl, fobs))
-    ek0, ek1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ek0.record()
-    if kgraph is not None:
-        kgraph.replay()
-    else:
-        for _ in range(K):
-            env.step_into(params, obs, ret, te, tr, tl, fobs)
-    ek1.record()
-    torch.cuda.synchronize()
-    kern_ms = ek0.elapsed_time(ek1) / K
+    kstep = lambda: env.step_into(params, obs, ret, te, tr, tl, fobs)   # noqa: E731
+    kgraph = capture(kstep)[0] if use_graph else None
+    kern_ms = timed_graph(kgraph, kstep)
     del kgraph
 
     # the timed BB steps: K x (episode launch [+ return all_gather]).  RCCL collectives on device
@@ -320,8 +364,8 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         graph, gerr = capture(lambda: bb_step())
         if gerr:
             print(f"[bench] graph capture failed ({gerr}); timing eager launches", file=sys.stderr)
-    n_captured = n_gathers[0] - W
-    n_gathers[0] = 0
+    n_captured = st["gathers"]
+    st["gathers"] = 0
     acc.zero_()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
@@ -331,10 +375,11 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     ev0.record()
     if graph is not None:
         graph.replay()
-        n_gathers[0] = n_captured
+        st["gathers"] = n_captured
     else:
         for _ in range(K):
             bb_step()
+        join()
     ev1.record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0          # closing barrier below is outside this window
@@ -346,7 +391,8 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         barrier_ms = (time.perf_counter() - tb) * 1e3
     inner_local = int(acc.sum().item())
     coll_ms = max(0.0, step_ms - kern_ms) if dist is not None else 0.0
-    timing_local = [kern_ms, step_ms, coll_ms, barrier_ms, elapsed * 1e3, float(n_gathers[0])]
+    timing_local = [kern_ms, step_ms, coll_ms, barrier_ms, elapsed * 1e3, float(st["gathers"]),
+                    -1.0 if gather_ms is None else gather_ms]
     if dist is not None:
         elapsed = shard.max_over_ranks(elapsed, coll_dev)
         inner = shard.sum_over_ranks(inner_local, coll_dev)
@@ -356,14 +402,16 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         inner = inner_local
         shards = [[lo, lo + N, inner_local]]
         timing = [timing_local]
-    per_rank = [{"rank": i, "kernel_ms_per_step": t[0], "step_ms": t[1], "collective_ms_per_step": t[2],
-                 "barrier_ms": t[3], "wall_ms": t[4], "gathers": int(t[5])} for i, t in enumerate(timing)]
+    per_rank = [{"rank": i, "kernel_ms_per_step": t[0], "step_ms": t[1], "exposed_collective_ms_per_step": t[2],
+                 "gather_ms": None if t[6] < 0 else t[6], "barrier_ms": t[3], "wall_ms": t[4], "gathers": int(t[5])}
+                for i, t in enumerate(timing)]
     launch = "hip graph of the K steps" if graph is not None else "eager"
     if gbuf is not None:
-        launch += (" (episode kernel + RCCL all_gather of the returns per BB step, captured)" if graph is not None
-                   else " (episode kernel + return all_gather per BB step)")
+        launch += " (episode kernel + return all_gather per BB step"
+        launch += (", gather k overlapped with episode k + 1 on a side stream" if overlap else ", in line")
+        launch += (", captured)" if graph is not None else ")")
     return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
-                shards=shards, per_rank=per_rank, launch=launch, gathers=n_gathers[0], capture_error=gerr)
+                shards=shards, per_rank=per_rank, launch=launch, gathers=st["gathers"], capture_error=gerr)
 
 
 def roofline(env_id, env, N, kern_ms, inner_local, K, simds, build_id):
@@ -436,6 +484,9 @@ def main():
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch the K steps eagerly instead of replaying them as one HIP graph")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="run each BB step's return all_gather in line after its episode kernel instead of "
+                         "overlapping it with the next step's kernel on a side stream")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the process group (and run the return gather) even for one rank: "
                          "exercises the RCCL path on a one-GPU box (tests/test_gpu_rccl.py)")
@@ -487,10 +538,10 @@ def main():
     else:
         n_local = args.envs
     K, W = args.steps, args.warmup
-    r = run_shard(args.env_id, n_local, rank, world, K, W, args.graph, dev, dist, coll_dev)
+    r = run_shard(args.env_id, n_local, rank, world, K, W, args.graph, dev, dist, coll_dev, args.overlap)
     weak = None
     if strong and world > 1 and not args.no_weak:   # secondary: 65536 envs per GPU
-        w = run_shard(args.env_id, GLOBAL_ENVS, rank, world, K, W, args.graph, dev, dist, coll_dev)
+        w = run_shard(args.env_id, GLOBAL_ENVS, rank, world, K, W, args.graph, dev, dist, coll_dev, args.overlap)
         weak = {"envs_per_gpu": GLOBAL_ENVS, "global_envs": GLOBAL_ENVS * world, "value": w["inner"] / w["elapsed"],
                 "ms_per_step": w["elapsed"] / K * 1e3, "kernel": w["env"].episode_kernel(),
                 "kernel_ms": w["kern_ms"]}
@@ -529,7 +580,10 @@ def main():
             # number of return gathers inside the timed region (= steps when N > 1)
             "timing": {"kernel_ms_per_step_max": max(t["kernel_ms_per_step"] for t in r["per_rank"]),
                        "step_ms_max": max(t["step_ms"] for t in r["per_rank"]),
-                       "collective_ms_per_step_max": max(t["collective_ms_per_step"] for t in r["per_rank"]),
+                       "exposed_collective_ms_per_step_max": max(t["exposed_collective_ms_per_step"]
+                                                                 for t in r["per_rank"]),
+                       "gather_ms_max": max((t["gather_ms"] for t in r["per_rank"] if t["gather_ms"] is not None),
+                                            default=None),
                        "barrier_ms_max": max(t["barrier_ms"] for t in r["per_rank"]),
                        "gathers": r["gathers"],
                        "per_rank": r["per_rank"]},

@@ -42,6 +42,7 @@ def test_bench_json_line():
     _check_roofline(d["roofline"])
     # 4096 envs x 200 inner steps per BB step (SimpleReacher never terminates early)
     assert d["value"] == pytest.approx(4096 * 200 / (d["ms_per_step"] * 1e-3), rel=1e-6)
+    assert d["timing"]["gathers"] == 0      # one rank, no process group: nothing to gather
 
 
 @pytest.mark.gpu

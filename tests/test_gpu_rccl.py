@@ -49,9 +49,10 @@ def test_bench_rccl_branch_one_rank():
     t = d["timing"]
     assert len(t["per_rank"]) == 1
     pr = t["per_rank"][0]
-    assert pr["kernel_ms_per_step"] > 0 and pr["collective_ms_per_step"] >= 0 and pr["barrier_ms"] >= 0
+    assert pr["kernel_ms_per_step"] > 0 and pr["exposed_collective_ms_per_step"] >= 0 and pr["barrier_ms"] >= 0
     assert pr["step_ms"] * 3 <= pr["wall_ms"] * 1.001
     # one RCCL return all_gather per timed BB step, captured in the HIP graph
     assert pr["gathers"] == 3 and t["gathers"] == 3
     assert "capture_error" not in t, t.get("capture_error")
-    assert "captured" in d["config"]["launch"]
+    assert "captured" in d["config"]["launch"] and "overlapped" in d["config"]["launch"]
+    assert pr["gather_ms"] > 0      # the captured all_gather timed alone
