@@ -245,7 +245,7 @@ def _cpu_worker(args):
 
 
 # ----------------------------------------------------------------------------- GPU run
-def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev, overlap=True):
+def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev, overlap="auto"):
     """K timed BB steps of this rank's shard (global envs [rank * n_local, (rank + 1) * n_local)),
     bracketed by barrier + synchronize on both sides.  Returns wall time (max over ranks), inner
     steps (sum over ranks), this rank's event time per step, inner steps and the env."""
@@ -269,28 +269,30 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     tl = torch.empty(N, dtype=torch.int32, device=dev)
     acc = env.new_inner_steps()   # device counter of inner env steps
     # every BB step ends with the episode-return all_gather over RCCL/xGMI (the path's only
-    # exchange): one all_gather_into_tensor of this rank's [N] f64 returns.
-    # On device buffers (RCCL) the returns are double-buffered and the gather of step k runs on a
-    # side stream while the episode kernel of step k + 1 runs (it reads nothing the gather
-    # writes); step k + 2 waits for gather k before it overwrites that return buffer.  The gloo
-    # rehearsal (host buffers) gathers in line.
+    # exchange): one all_gather_into_tensor of this rank's [N] f64 returns.  Two
+    # schedules of the same work: "inline" (the gather follows its episode kernel on the launch
+    # stream) and "overlap" (returns double-buffered, gather k on a side stream while episode
+    # k + 1 runs; step k + 2 waits for gather k before it overwrites that buffer).  With
+    # --overlap auto both are captured, each replayed once untimed, and the one whose slowest
+    # rank is faster is timed (the same choice on every rank).  The gloo rehearsal (host buffers)
+    # gathers in line, eagerly.
     gbuf = torch.empty(N * world, dtype=torch.float64, device=coll_dev) if dist is not None else None
-    overlap = overlap and gbuf is not None and gbuf.is_cuda
-    rets = [ret, torch.empty_like(ret)] if overlap else [ret, ret]
-    gbufs = [gbuf, torch.empty_like(gbuf)] if overlap else [gbuf, gbuf]
-    comm = torch.cuda.Stream(device=dev) if overlap else None
+    can_overlap = gbuf is not None and gbuf.is_cuda and overlap != "off"
+    rets = [ret, torch.empty_like(ret)] if can_overlap else [ret, ret]
+    gbufs = [gbuf, torch.empty_like(gbuf)] if can_overlap else [gbuf, gbuf]
+    comm = torch.cuda.Stream(device=dev) if can_overlap else None
     st = {"k": 0, "gathers": 0, "free": [None, None], "pending": False}
 
-    def bb_step(count=True):
-        s = st["k"] % 2
+    def bb_step(ov, count=True):
+        s = st["k"] % 2 if ov else 0
         st["k"] += 1
-        if overlap and st["free"][s] is not None:
+        if ov and st["free"][s] is not None:
             torch.cuda.current_stream().wait_event(st["free"][s])
         env.step_into(params, obs, rets[s], te, tr, tl, fobs, inner_steps=acc if count else None)
         if gbuf is None:
             return
         st["gathers"] += 1
-        if not overlap:
+        if not ov:
             shard.gather_returns_into(gbufs[s], rets[s])
             return
         ready = torch.cuda.Event()
@@ -310,8 +312,7 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         st["free"], st["pending"] = [None, None], False
 
     for _ in range(W):
-        bb_step(count=False)
-    join()
+        bb_step(False, count=False)
     torch.cuda.synchronize()
     st["gathers"] = 0
 
@@ -359,12 +360,34 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     # the timed BB steps: K x (episode launch [+ return all_gather]).  RCCL collectives on device
     # buffers are captured into the same HIP graph as the kernels; the gloo rehearsal (host
     # buffers) cannot be captured and runs eagerly.
-    graph, gerr = None, None
+    graph, gerr, ov = None, None, overlap == "on" and can_overlap
+    trial = {}
     if use_graph and (gbuf is None or gbuf.is_cuda):
-        graph, gerr = capture(lambda: bb_step())
-        if gerr:
+        modes = [False, True] if (overlap == "auto" and can_overlap) else [ov]
+        graphs = {}
+        for m in modes:
+            st["gathers"] = 0
+            g, e = capture(lambda: bb_step(m))
+            if g is None:
+                gerr = e
+                continue
+            graphs[m] = (g, st["gathers"])
+        if len(graphs) == 2:   # one untimed replay of each, slowest rank decides, same pick everywhere
+            t_in = timed_graph(graphs[False][0], None)
+            t_ov = timed_graph(graphs[True][0], None)
+            if dist is not None:
+                t_in, t_ov = [max(x) for x in zip(*shard.gather_floats([t_in, t_ov], coll_dev))]
+            trial = {"inline_ms_per_step": t_in, "overlap_ms_per_step": t_ov}
+            ov = t_ov < t_in
+        elif graphs:
+            ov = next(iter(graphs))
+        if graphs:
+            graph, n_captured = graphs[ov]
+            graphs.clear()
+        elif gerr:
             print(f"[bench] graph capture failed ({gerr}); timing eager launches", file=sys.stderr)
-    n_captured = st["gathers"]
+    if graph is None:
+        n_captured = 0
     st["gathers"] = 0
     acc.zero_()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -378,7 +401,7 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
         st["gathers"] = n_captured
     else:
         for _ in range(K):
-            bb_step()
+            bb_step(ov)
         join()
     ev1.record()
     torch.cuda.synchronize()
@@ -408,10 +431,11 @@ def run_shard(env_id, n_local, rank, world, K, W, use_graph, dev, dist, coll_dev
     launch = "hip graph of the K steps" if graph is not None else "eager"
     if gbuf is not None:
         launch += " (episode kernel + return all_gather per BB step"
-        launch += (", gather k overlapped with episode k + 1 on a side stream" if overlap else ", in line")
+        launch += (", gather k overlapped with episode k + 1 on a side stream" if ov else ", in line")
         launch += (", captured)" if graph is not None else ")")
     return dict(elapsed=elapsed, inner=inner, inner_local=inner_local, kern_ms=kern_ms, env=env, params=params,
-                shards=shards, per_rank=per_rank, launch=launch, gathers=st["gathers"], capture_error=gerr)
+                shards=shards, per_rank=per_rank, launch=launch, gathers=st["gathers"], capture_error=gerr,
+                schedule_trial=trial)
 
 
 def roofline(env_id, env, N, kern_ms, inner_local, K, simds, build_id):
@@ -484,9 +508,10 @@ def main():
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="launch the K steps eagerly instead of replaying them as one HIP graph")
-    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
-                    help="run each BB step's return all_gather in line after its episode kernel instead of "
-                         "overlapping it with the next step's kernel on a side stream")
+    ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
+                    help="N > 1 (RCCL): run each BB step's return all_gather in line after its episode kernel "
+                         "(off), overlapped with the next step's kernel on a side stream (on), or time both "
+                         "once untimed and keep the faster (auto)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise the process group (and run the return gather) even for one rank: "
                          "exercises the RCCL path on a one-GPU box (tests/test_gpu_rccl.py)")
@@ -589,6 +614,8 @@ def main():
                        "per_rank": r["per_rank"]},
             "roofline": roofline(args.env_id, env, n_local, r["kern_ms"], r["inner_local"], K, simds, lib_build_id()),
         }
+        if r["schedule_trial"]:
+            line["timing"]["schedule_trial"] = r["schedule_trial"]
         if r["capture_error"]:
             line["timing"]["capture_error"] = r["capture_error"]
         if weak is not None:

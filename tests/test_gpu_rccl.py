@@ -54,5 +54,10 @@ def test_bench_rccl_branch_one_rank():
     # one RCCL return all_gather per timed BB step, captured in the HIP graph
     assert pr["gathers"] == 3 and t["gathers"] == 3
     assert "capture_error" not in t, t.get("capture_error")
-    assert "captured" in d["config"]["launch"] and "overlapped" in d["config"]["launch"]
+    assert "captured" in d["config"]["launch"]
+    # --overlap auto: both schedules replayed once untimed, the faster one timed
+    tr = t["schedule_trial"]
+    assert tr["inline_ms_per_step"] > 0 and tr["overlap_ms_per_step"] > 0
+    picked_overlap = "overlapped" in d["config"]["launch"]
+    assert picked_overlap == (tr["overlap_ms_per_step"] < tr["inline_ms_per_step"])
     assert pr["gather_ms"] > 0      # the captured all_gather timed alone
