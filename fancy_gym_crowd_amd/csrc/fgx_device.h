@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "fgx_rng.h"
 #include "fgx_trig.h"
 
@@ -19,6 +22,24 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // read-only table memory in the constant address space: a wave-uniform address is loaded with
 // s_load into SGPRs (the scalar cache), not per lane through LDS / VMEM
 typedef const float __attribute__((address_space(4)))* cfloat_ptr;
+
+// Host: a launch with more than 64 KB of dynamic LDS needs the kernel's limit raised first.  The
+// limit is raised once per kernel (to the largest size asked for so far) and cached, so the
+// per-step launches do not pay a hipFuncSetAttribute each.
+inline hipError_t raise_lds_limit(const void* kernel, size_t lds) {
+  if (lds <= 64 * 1024) return hipSuccess;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> raised[64];   // per device ordinal
+  if (dev < 0 || dev >= 64) return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& have = raised[dev][kernel];
+  if (have >= lds) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) have = lds;
+  return e;
+}
 
 constexpr int kMaxLinks = 8;
 constexpr int kMaxObs = 3 * kMaxLinks + 5;

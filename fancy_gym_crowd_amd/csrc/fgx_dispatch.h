@@ -160,9 +160,7 @@ static int launch_jp(const DevCfg& c, const DevState& s, const float* params, co
     err = "k_episode_jp: basis table too large for LDS";
     return -4;
   }
-  if (lj > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)k_episode_jp<MP, NL, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lj) != hipSuccess) {
+  if (raise_lds_limit((const void*)k_episode_jp<MP, NL, NB>, lj) != hipSuccess) {
     err = "k_episode_jp: cannot raise the dynamic LDS limit";
     return -2;
   }
@@ -181,9 +179,7 @@ static int launch_ws(const DevCfg& c, const DevState& s, const float* params, co
     err = "k_episode_ws: basis table too large for LDS";
     return -4;
   }
-  if (lw > 64 * 1024 &&
-      hipFuncSetAttribute((const void*)k_episode_ws<MP, NL, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lw) != hipSuccess) {
+  if (raise_lds_limit((const void*)k_episode_ws<MP, NL, NB>, lw) != hipSuccess) {
     err = "k_episode_ws: cannot raise the dynamic LDS limit";
     return -2;
   }
@@ -217,8 +213,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     const int k = episode_kernel_choice(c, MP, log, s.plan_len != nullptr);
     if (k == EK_V2) {
       const size_t lv = v2_lds_bytes(c.rows, c.stride, NL);
-      if (lv > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_v2<MP, NL, NB>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lv) != hipSuccess) {
+      if (raise_lds_limit((const void*)k_episode_v2<MP, NL, NB>, lv) != hipSuccess) {
         err = "k_episode_v2: cannot raise the dynamic LDS limit";
         return -2;
       }
@@ -255,8 +250,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
   if constexpr (!LOG_ONLY && ENV != ENV_SIMPLE) {
     if (v2h_applies(c, log)) {
       const size_t lh = v2h_lds_bytes(MP, c.rows, c.stride, NL, c.full_dim);
-      if (lh > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_v2h<ENV, MP, CTRL, NL, NB>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lh) != hipSuccess) {
+      if (raise_lds_limit((const void*)k_episode_v2h<ENV, MP, CTRL, NL, NB>, lh) != hipSuccess) {
         err = "k_episode_v2h: cannot raise the dynamic LDS limit";
         return -2;
       }
@@ -274,9 +268,7 @@ static int launch_episode_nl(const DevCfg& c, const DevState& s, const float* pa
     }
     // + the four waves' info staging regions (InfoStage, fgx_device.h)
     const size_t ll = stage_tab_offset(lds / sizeof(float)) + (threads / 64) * stage_wave_bytes(NL, c.full_dim);
-    if (ll > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)k_episode<ENV, MP, CTRL, NL, NB, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ll) != hipSuccess) {
+    if (raise_lds_limit((const void*)k_episode<ENV, MP, CTRL, NL, NB, true>, ll) != hipSuccess) {
       err = "k_episode (info rows): cannot raise the dynamic LDS limit";
       return -2;
     }

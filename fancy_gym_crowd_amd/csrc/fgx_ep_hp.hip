@@ -12,8 +12,7 @@ static int launch_hp(const DevCfg& c, const DevState& s, const float* params, co
     return -1;
   }
   const size_t lds = hp_lds_bytes(5, G);
-  if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_episode_hp<MP, CTRL, 5, 5, G, INFO>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+  if (raise_lds_limit((const void*)k_episode_hp<MP, CTRL, 5, 5, G, INFO>, lds) != hipSuccess) {
     err = "k_episode_hp: cannot raise the dynamic LDS limit";
     return -2;
   }

@@ -29,7 +29,9 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
   return 0;
 }
 
-// the helper form (fgx_jl.h, HLP 1 / 2): ProMP on the column table; FGX_JL_HELPER=0 / 1 / 2 forces
+// the helper form (fgx_jl.h, HLP 1 / 2): ProMP on the column table, measured slower than the plain
+// form and compiled only into diagnostics builds (-DFGX_JL_HELPER_FORM,
+// _build.build_variant); FGX_JL_HELPER=1 / 2 selects it there and is refused by the release build
 inline int jl_helper(const fgx::DevCfg& c) {
   if (const char* v = std::getenv("FGX_JL_HELPER")) return v[0] == '1' ? 1 : v[0] == '2' ? 2 : 0;
   (void)c;
@@ -39,15 +41,23 @@ inline int jl_helper(const fgx::DevCfg& c) {
 template <int MP, int NB>
 int launch_jl_nl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
                  hipStream_t stream, std::string& err) {
-  if constexpr (MP == fgx::MP_PROMP && NB == 5) {
-    const int h = jl_helper(c);
-    if (h == 1) {
-      if (c.nl == 2) return launch_jl<MP, 2, NB, 1>(c, s, params, o, stream, err);
-      if (c.nl == 5) return launch_jl<MP, 5, NB, 1>(c, s, params, o, stream, err);
-    } else if (h == 2) {
-      if (c.nl == 2) return launch_jl<MP, 2, NB, 2>(c, s, params, o, stream, err);
-      if (c.nl == 5) return launch_jl<MP, 5, NB, 2>(c, s, params, o, stream, err);
+  if (const int h = jl_helper(c)) {
+#ifdef FGX_JL_HELPER_FORM
+    if constexpr (MP == fgx::MP_PROMP && NB == 5) {
+      if (h == 1) {
+        if (c.nl == 2) return launch_jl<MP, 2, NB, 1>(c, s, params, o, stream, err);
+        if (c.nl == 5) return launch_jl<MP, 5, NB, 1>(c, s, params, o, stream, err);
+      } else {
+        if (c.nl == 2) return launch_jl<MP, 2, NB, 2>(c, s, params, o, stream, err);
+        if (c.nl == 5) return launch_jl<MP, 5, NB, 2>(c, s, params, o, stream, err);
+      }
     }
+#else
+    (void)h;
+    err = "k_episode_jl: FGX_JL_HELPER asks for the helper form, which this build does not contain "
+          "(a diagnostics build with -DFGX_JL_HELPER_FORM does)";
+    return -4;
+#endif
   }
   if (c.nl == 2) return launch_jl<MP, 2, NB>(c, s, params, o, stream, err);
   if (c.nl == 5) return launch_jl<MP, 5, NB>(c, s, params, o, stream, err);

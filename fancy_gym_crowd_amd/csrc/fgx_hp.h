@@ -530,7 +530,7 @@ inline size_t hp_lds_bytes(int nl, int groups) {
 }
 static_assert(4 * HpLayout<5>::GROUP * sizeof(double) <= 160 * 1024, "k_episode_hp: four groups fit one CU's LDS");
 
-// k_episode_hp serves this step (FGX_HP=0 or FGX_EPISODE_KERNEL=classic|pair keep the others: A/B, tests)
+// k_episode_hp serves this step (FGX_HP=0 or any FGX_EPISODE_KERNEL but "hp" keep the others: A/B, tests)
 // log: some per-step array is written (the INFO instantiation; FGX_V2=0 keeps the logging k_episode)
 // heavy: the verbose-2 rows (planned positions / velocities, step observations): k_episode_v2h stays
 // faster there (65536 envs: 1026 vs 1637 us, profiles/r05_s9_jlhelper_traj_hpinfo.jsonl), so k_episode_hp takes
@@ -542,8 +542,9 @@ inline bool hp_applies(const DevCfg& c, const DevState& s, int mp, bool log, boo
     force = std::strcmp(v, "1") == 0;
   }
   if (heavy && !force) return false;
+  // a forced kernel wins (fgx_dispatch.h): any FGX_EPISODE_KERNEL other than "hp" keeps k_episode_hp out
   if (const char* v = std::getenv("FGX_EPISODE_KERNEL"))
-    if (std::strcmp(v, "classic") == 0 || std::strcmp(v, "pair") == 0) return false;
+    if (*v && std::strcmp(v, "hp") != 0) return false;
   if (log)
     if (const char* v = std::getenv("FGX_V2"))
       if (std::strcmp(v, "0") == 0) return false;

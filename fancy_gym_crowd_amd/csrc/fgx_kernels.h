@@ -868,7 +868,8 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     if (k_replan >= 0) Lp = min(Lp, k_replan + 1);
     split = (Lp > 128) ? ((Lp / 2) & ~7) : 0;
   }
-  double* rew_row = ((ENV != ENV_SIMPLE || c.sched_state) && s.rew) ? s.rew + e : nullptr;
+  // only read back for segments longer than 128 samples (L <= T): shorter plans store nothing
+  double* rew_row = ((ENV != ENV_SIMPLE || c.sched_state) && s.rew && c.T > 128) ? s.rew + e : nullptr;
   bool term = false, trunc = false, stop = false;
   float pos[NL], vel[NL];
   // fast blocks are software-pipelined: sample k's f64 controller / dynamics and the f32

@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64 * kTrajGWaves) void k_traj_mfma(DevCfg c, DevSta
 // a launch with more than 64 KB of dynamic LDS needs the kernel's limit raised first
 template <typename F>
 inline void launch_lds(const void* kernel, size_t lds, F&& launch) {
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)raise_lds_limit(kernel, lds);
   launch();
 }
 

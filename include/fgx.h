@@ -274,7 +274,11 @@ int fgx_get_tables(void* handle, float* out, void* stream);
  * info_level >= 1 means some per-step output pointer is given (the launch then runs k_episode_hp, the
  * logging k_episode, k_episode_v2 or k_episode_v2h, as it does for a config with valid_flags; 2: the
  * verbose-2 rows, planned positions and step observations included).  All nine give
- * bit-identical results; the choice follows measured speed (fgx_dispatch.h, fgx_hp.h). */
+ * bit-identical results; the choice follows measured speed (fgx_dispatch.h, fgx_hp.h).
+ * The report is for fgx_step with the handle's own plans and the output sets the Python VectorEnv
+ * passes at that level (level >= 2: positions and step observations given, which is the launch's
+ * "heavy" predicate); fgx_step_traj (caller-supplied plans) and C callers passing other subsets of
+ * the per-step arrays may launch a different kernel of the same nine. */
 int fgx_episode_kernel(void* handle, int32_t info_level);
 
 /* Diagnostics (tests): for x[0..n) (device f64), out[4 n] = {sin, cos} of the kernels' sincos

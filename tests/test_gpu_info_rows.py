@@ -205,9 +205,11 @@ def _hp_or_v2h(a, kern, info_level=2):
     return k
 
 
-@pytest.mark.parametrize("kern", ["default", "v2h", "hp"])
-@pytest.mark.parametrize("N", [512, 1024])
-@pytest.mark.parametrize("info_level", [1, 2])
+# FGX_HP=1 only changes the level-2 dispatch, so "hp" runs at level 2 and one size only
+V2H_KERNS = [(k, lvl, n) for k in ("default", "v2h") for lvl in (1, 2) for n in (512, 1024)] + [("hp", 2, 512)]
+
+
+@pytest.mark.parametrize("kern,info_level,N", V2H_KERNS)
 @pytest.mark.parametrize("ci", range(len(V2H_CASES)))
 def test_v2h_equals_logging_kernel(ci, info_level, N, kern, monkeypatch):
     """k_episode_v2h (fgx_kernels.h: the logging body on waves 0..3, its per-step rows stored by waves
@@ -215,8 +217,6 @@ def test_v2h_equals_logging_kernel(ci, info_level, N, kern, monkeypatch):
     whole device state bit for bit over 6 BB steps with collisions (terminations at every sample),
     auto-resets and replanning segments."""
     env_id, over, kw = V2H_CASES[ci]
-    if kern == "hp" and (info_level < 2 or N != 512):
-        pytest.skip("FGX_HP=1 only changes the level-2 dispatch (one size)")
     if kern != "default":
         monkeypatch.setenv("FGX_HP", "0" if kern == "v2h" else "1")
     a = fgx.make(env_id, num_envs=N, device=DEV, mp_config_override=over, info_level=info_level, **kw)

@@ -161,48 +161,14 @@ def test_jl_equals_classic_split_autoreset(N, monkeypatch):
     _same(outs[0], outs[1])
 
 
-HELPER_CASES = [
-    # (env id, mp_config_override, N, BB steps, restored steps)
-    ("fancy_ProMP/LongSimpleReacher-v0", None, 8192, 2, False),      # the 8-GPU shard: every wave fast
-    ("fancy_ProMP/LongSimpleReacher-v0", None, 61, 2, False),        # one partial workgroup, idle lanes
-    ("fancy_ProMP/LongSimpleReacher-v0", None, 1000, 3, True),       # envs at every step: mixed waves
-    ("fancy_ProMP/SimpleReacher-v0", None, 4097, 2, False),          # 2 links (32 envs per wave)
-    ("fancy_ProMP/LongSimpleReacher-v0", {"black_box_kwargs": {"replanning_schedule": fgx.ReplanEvery(40),
-                                                               "condition_on_desired": True}}, 300, 6, False),
-]
-
-
-@pytest.mark.parametrize("hv", ["1", "2"])
-@pytest.mark.parametrize("ci", range(len(HELPER_CASES)))
-def test_jl_helper_equals_jl(ci, hv, monkeypatch):
-    """k_episode_jl's helper forms (FGX_JL_HELPER=1 / 2: one joint wave + one helper wave per workgroup,
-    the trajectory chunks and the pairwise reduction on the helper, fgx_jl.h HLP) against the plain
-    joint-lane kernel: every output and the device state bit for bit, with NaN / inf / huge
-    parameters in some envs (their waves leave the fast path: the helper idles) and the split
-    auto-reset running on the helper wave's threads."""
-    env_id, over, N, n_bb, restored = HELPER_CASES[ci]
-    probe = fgx.make(env_id, num_envs=8, device=DEV, info_level=0, mp_config_override=over)
-    rng = np.random.default_rng(300 + ci)
-    params = [rng.standard_normal((N, probe.n_params), dtype=np.float32) for _ in range(n_bb)]
-    if N > 100:
-        params[0][7, 2] = np.nan
-        params[1][50, 0] = np.inf
-        params[-1][90, :] = 3e4
-    del probe
-    outs = []
-    for h in (hv, "0"):
-        monkeypatch.setenv("FGX_JL_HELPER", h)
-        monkeypatch.setenv("FGX_EPISODE_KERNEL", "jl")
-        env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, mp_config_override=over, random_start=False)
-        assert kernel_is(env.episode_kernel(), "k_episode_jl")
-        out = [np_(env.reset(seed=29)[0])]
-        if restored:
-            env.set_state(steps=(np.arange(N) * 7 % 200).astype(np.int32))
-        for p in params:
-            obs, ret, te, tr, info = env.step(torch.from_numpy(p).to(DEV))
-            out += [np_(obs), np_(ret), np_(te), np_(tr), np_(info["trajectory_length"]),
-                    np_(info["final_observation"])]
-            out += list(_state(env).values())
-        outs.append(out)
-    _same(outs[0], outs[1])
+def test_jl_helper_form_not_in_release_build(monkeypatch):
+    """k_episode_jl's helper form (fgx_jl.h HLP; measured slower) is compiled only into
+    diagnostics builds (-DFGX_JL_HELPER_FORM): asking the release library for it is an error, not a
+    silent fallback to the plain kernel."""
+    monkeypatch.setenv("FGX_JL_HELPER", "1")
+    monkeypatch.setenv("FGX_EPISODE_KERNEL", "jl")
+    env = fgx.make("fancy_ProMP/LongSimpleReacher-v0", num_envs=64, device=DEV, info_level=0)
+    env.reset(seed=1)
+    with pytest.raises(ValueError, match="helper form"):
+        env.step(torch.zeros((64, env.n_params), device=DEV))
 

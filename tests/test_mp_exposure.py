@@ -34,8 +34,13 @@ def test_exposure_small_batch():
     assert s["max_return_rel_dev"] < 1e-5
 
 
+# committed bound per BB step on the observation values outside the north-star tolerance (rtol 1e-5,
+# atol 1e-6) under f32 MP tables: config 3 <= 4, the metric <= 1 (profiles/r06_mp_f32_exposure.json)
+OBS_OUTSIDE_TOL_MAX = {"config3": 4, "metric": 1}
+
+
 def test_committed_full_size_result():
-    with open(os.path.join(ROOT, "profiles", "r05_mp_f32_exposure.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r06_mp_f32_exposure.json")) as f:
         res = json.load(f)["results"]
     assert {r["config"] for r in res} == {"config3", "metric"}
     for r in res:
@@ -43,3 +48,18 @@ def test_committed_full_size_result():
         for s in r["steps"]:
             assert s["length_flips"] == 0 and s["terminated_flips"] == 0 and s["truncated_flips"] == 0
             assert s["max_return_rel_dev"] < 1e-5 and np.isfinite(s["max_obs_abs_dev"])
+            assert s["obs_outside_tol"] <= OBS_OUTSIDE_TOL_MAX[r["config"]]
+            assert len(s["obs_outliers"]) == s["obs_outside_tol"]
+            for o in s["obs_outliers"]:
+                # every outlier is a small value where the absolute tolerance binds, off by < 5e-6
+                assert o["atol_binds"] and abs(o["f64_tables"]) < 0.1 and o["abs_dev"] < 5e-6, o
+                assert o["name"] in ("qdot0", "ee_minus_goal_y"), o
+
+
+def test_outliers_are_named():
+    """tools/mp_f32_exposure.obs_outliers names each value outside the tolerance and says whether the
+    absolute tolerance binds there"""
+    a = np.array([[0.05, 2.0, 1.0]], np.float32)
+    b = np.array([[0.050003, 2.0, 1.00002]], np.float32)
+    out = mx.obs_outliers(a, b, ["qdot0", "x", "y"])
+    assert [(o["name"], o["atol_binds"]) for o in out] == [("qdot0", True), ("y", False)]

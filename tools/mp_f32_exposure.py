@@ -153,6 +153,34 @@ def run_oracle(name, ctrl, spec, tables, kw, plist, N, workers, chunks):
     return [tuple(np.concatenate([res[lo][b][f] for lo in sorted(res)]) for f in range(6)) for b in range(len(plist))]
 
 
+def obs_names(env):
+    """column names of the oracle's observation (oracle/batched.py obs(), then the context mask)"""
+    n = env.n
+    names = [f"cos_q{i}" for i in range(n)] + [f"sin_q{i}" for i in range(n)] + [f"qdot{i}" for i in range(n)]
+    if env.kind == "hole":
+        names.append("hole_width")
+    if env.kind == "via":
+        names += ["ee_minus_via_x", "ee_minus_via_y"]
+    names += ["ee_minus_goal_x", "ee_minus_goal_y", "steps"]
+    mask = getattr(env, "mask", None)
+    return [nm for nm, m in zip(names, mask)] if mask is not None else names
+
+
+def obs_outliers(fa, fb, names, rtol=1e-5, atol=1e-6):
+    """every observation value outside the parity tolerance: env, column, both values and whether
+    it is a near-zero value where atol binds (|a| * rtol < atol, i.e. |a| < 0.1)"""
+    a64, b64 = fa.astype(np.float64), fb.astype(np.float64)
+    dev = np.abs(a64 - b64)
+    bad = np.argwhere(dev > rtol * np.abs(a64) + atol)
+    out = []
+    for e, j in bad:
+        a, b = float(a64[e, j]), float(b64[e, j])
+        out.append(dict(env=int(e), col=int(j), name=names[j] if j < len(names) else f"col{j}", f64_tables=a,
+                        f32_tables=b, abs_dev=float(dev[e, j]), rel_dev=float(dev[e, j] / max(abs(a), 1e-300)),
+                        atol_binds=bool(abs(a) * rtol < atol)))
+    return out
+
+
 def exposure(cfg_name, N, n_bb, workers=8, chunks=16):
     import fancy_gym_crowd_amd as fgx
     env_id, name = CONFIGS[cfg_name]
@@ -169,6 +197,7 @@ def exposure(cfg_name, N, n_bb, workers=8, chunks=16):
     a = run_oracle(name, ctrl, spec, t64, kw, plist, N, workers, chunks)
     b = run_oracle(name, ctrl, spec, t32, kw, plist, N, workers, chunks)
     steps = []
+    names = obs_names(batched.BatchedBB(name, 1, ctrl, mp_spec=spec, tables=t64, **kw).env)
     for s in range(n_bb):
         la, ta, ra, reta, oa, fa = a[s]
         lb, tb, rb, retb, obb, fb = b[s]
@@ -191,6 +220,7 @@ def exposure(cfg_name, N, n_bb, workers=8, chunks=16):
             obs_outside_tol=int((np.abs(fa.astype(np.float64) - fb.astype(np.float64)) >
                                  1e-5 * np.abs(fa.astype(np.float64)) + 1e-6).sum()),
             obs_values=int(fa.size),
+            obs_outliers=obs_outliers(fa, fb, names),
         ))
     return dict(config=cfg_name, env_id=env_id, envs=N, bb_steps=n_bb, tables=table_deviation(t64, t32),
                 steps=steps, seconds=round(time.time() - t0, 1))
