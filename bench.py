@@ -205,12 +205,22 @@ def cpu_baseline(seconds=12.0, cores=None):
         wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
     per_core = float(np.mean([r[0] / r[1] for r in res]))
+    calib, cal_note = None, "no committed calibration"
+    try:   # tools/cpu_calibration.py: this worker vs the shimmed reference, one core, one process
+        with open(os.path.join(ROOT, "profiles", "r06_cpu_calibration.json")) as f:
+            cj = json.load(f)
+        calib = {k: cj[k] for k in ("reference_steps_per_s", "port_steps_per_s", "port_over_reference")}
+        calib["source"] = "profiles/r06_cpu_calibration.json (tools/cpu_calibration.py, build container)"
+        cal_note = (f"calibrated in the build container against the shimmed reference (stub MP): this worker runs "
+                    f"{cj['port_over_reference']:.3f}x the reference loop's rate on the same core")
+    except (OSError, ValueError, KeyError):
+        pass
     return dict(value=steps / wall, unit="inner env-steps/s", cores=cores, kind="port",
-                per_core=per_core, affinity_cpus=aff, cores_source=source,
+                per_core=per_core, affinity_cpus=aff, cores_source=source, calibration=calib,
                 sample=f"oracle/port.py per-env loop (f32 ProMP contraction + PD + 200 substeps with the "
                        f"reference's per-step numpy ops incl. its 2 self-collision checks + autoreset), "
                        f"{WORKLOAD}, {cores} processes x ~{seconds:.0f}s, {steps} inner steps; "
-                       f"os.cpu_count()={os.cpu_count()}, usable CPUs from {source}")
+                       f"os.cpu_count()={os.cpu_count()}, usable CPUs from {source}; {cal_note}")
 
 
 def _cpu_worker(args):
