@@ -121,7 +121,13 @@ struct DevState {
   const float* tables_t;
 };
 
-__host__ __device__ inline int tables_t_rows(int rows) { return (rows + 32 + 7) & ~7; }
+// rows per column: at least kTabTRows, so that k_episode_jl's chunk loads address their columns with
+// compile-time offsets from one base (no per-column 64-bit address arithmetic in the sample loop)
+constexpr int kTabTRows = 512;
+__host__ __device__ inline int tables_t_rows(int rows) {
+  const int r = (rows + 32 + 7) & ~7;
+  return r > kTabTRows ? r : kTabTRows;
+}
 // basis columns start their rows at offset 6 (a chunk reads rows k0 + 2 ..), the dt columns at 7
 // (rows k0 + 1 ..): both land on multiples of 8 for k0 % 8 == 0
 __host__ __device__ inline int tables_t_pad(int col, int nb) { return col < nb ? 6 : 7; }

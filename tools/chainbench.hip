@@ -26,9 +26,11 @@ constexpr int SAMPLES = 1600;
 #define CH_MAX(dst, a, b) asm volatile("v_max_f64 %0, %1, %2" : "=v"(dst) : "v"(a), "v"(b))
 #define CH_MIN(dst, a, b) asm volatile("v_min_f64 %0, %1, %2" : "=v"(dst) : "v"(a), "v"(b))
 #define IND(i) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(ind[(i) & 7]) : "v"(wa), "v"(wb))
+// a 64-bit scalar address advance (what the fast chunk does per scalar table load)
+#define SAL(i) asm volatile("s_add_u32 %0, %0, 32\n\ts_addc_u32 %1, %1, 0" : "+s"(sa[(i) & 3]), "+s"(sb[(i) & 3]) :: "scc")
 
 template <int MODE>
-__global__ __launch_bounds__(64) void k_chain(double* out, double pg, double dg, double dt, double lo, double hi,
+__global__ __launch_bounds__(512) void k_chain(double* out, double pg, double dg, double dt, double lo, double hi,
                                                float wseed) {
   const int e = blockIdx.x * 64 + threadIdx.x;
   double one = 1.0;
@@ -38,6 +40,7 @@ __global__ __launch_bounds__(64) void k_chain(double* out, double pg, double dg,
 #pragma unroll
   for (int i = 0; i < 8; ++i) ind[i] = f32x2{wseed + i, wseed - i};
   const f32x2 wa = {0.999f, 0.998f}, wb = {1e-3f, 2e-3f};
+  unsigned sa[4] = {1, 2, 3, 4}, sb[4] = {5, 6, 7, 8};
   for (int k = 0; k < SAMPLES; ++k) {
     double e1, e2, u1, u2, u, a, t1, t2;
     if constexpr (MODE == 1) {
@@ -67,22 +70,27 @@ __global__ __launch_bounds__(64) void k_chain(double* out, double pg, double dg,
 #pragma unroll
         for (int i = 0; i < 12; ++i) IND(i);
       }
+      if (MODE == 5) {   // chain + 4 scalar 64-bit address advances (8 SALU)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) SAL(i);
+      }
     }
   }
   float s = 0.0f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += ind[i].x + ind[i].y;
-  out[e] = q + qd + s;
+  out[e] = q + qd + s + (double)(sa[0] + sa[1] + sa[2] + sa[3] + sb[0] + sb[1] + sb[2] + sb[3]);
 }
 
 template <int MODE>
-static int run(double* out, int waves) {
+static int run(double* out, int waves, int threads = 64) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
   for (int rep = 0; rep < 2; ++rep) {   // warm-up launch, then the timed one
     CHK(hipEventRecord(a));
-    hipLaunchKernelGGL(k_chain<MODE>, dim3(waves), dim3(64), 0, 0, out, 0.6, 0.075, 0.01, -1.0, 1.0, 0.5f);
+    hipLaunchKernelGGL(k_chain<MODE>, dim3(waves * 64 / threads), dim3(threads), 0, 0, out, 0.6, 0.075, 0.01, -1.0, 1.0,
+                       0.5f);
     CHK(hipEventRecord(b));
     CHK(hipEventSynchronize(b));
   }
@@ -90,9 +98,11 @@ static int run(double* out, int waves) {
   CHK(hipEventElapsedTime(&ms, a, b));
   const char* names[] = {"chain only (13 f64, 9 dependent)", "12 independent pk_fma only", "chain then 12 independent",
                          "chain with 1 independent after each of its ops (12 total)",
-                         "chain with 2 independent after each of its first 6 ops (12 total)"};
-  printf("{\"mode\": %d, \"what\": \"%s\", \"waves\": %d, \"us\": %.2f, \"cycles_per_sample_at_2.4GHz\": %.1f}\n", MODE,
-         names[MODE], waves, ms * 1e3, ms * 1e-3 * 2.4e9 / SAMPLES);
+                         "chain with 2 independent after each of its first 6 ops (12 total)",
+                         "chain then 8 SALU (4 s_add_u32 / s_addc_u32 pairs)"};
+  printf("{\"mode\": %d, \"what\": \"%s\", \"waves\": %d, \"threads\": %d, \"us\": %.2f, "
+         "\"cycles_per_sample_at_2.4GHz\": %.1f}\n", MODE, names[MODE], waves, threads, ms * 1e3,
+         ms * 1e-3 * 2.4e9 / SAMPLES);
   return 0;
 }
 
@@ -100,7 +110,15 @@ int main() {
   double* out;
   const int waves = 1024;   // one wave per SIMD on 256 CUs
   CHK(hipMalloc(&out, sizeof(double) * 64 * waves));
-  if (run<0>(out, waves) || run<1>(out, waves) || run<2>(out, waves) || run<3>(out, waves) || run<4>(out, waves)) return 1;
+  CHK(hipFree(out));
+  CHK(hipMalloc(&out, sizeof(double) * 64 * waves * 2));
+  if (run<0>(out, waves) || run<1>(out, waves) || run<2>(out, waves) || run<3>(out, waves) || run<4>(out, waves) ||
+      run<5>(out, waves))
+    return 1;
+  // two waves per SIMD (2048 waves in 512-thread workgroups: waves w, w + 4 share a SIMD)
+  if (run<0>(out, 2 * waves, 512) || run<1>(out, 2 * waves, 512) || run<2>(out, 2 * waves, 512)) return 1;
+  // one wave per SIMD through 256-thread workgroups (4 waves per CU, one per SIMD)
+  if (run<2>(out, waves, 256)) return 1;
   CHK(hipFree(out));
   return 0;
 }
