@@ -119,7 +119,12 @@ struct DevState {
   // j * RT + r + tables_t_pad(j, nb) (k_episode_jl's ProMP chunks load 8 consecutive rows of one
   // column with one 32-byte-aligned scalar load)
   const float* tables_t;
+  // per-sample windows of the shared table for k_episode's level-scheduled ProMP samples (5 basis
+  // functions): window r = 16 floats {dt_r, 0, 1/dt_r, 0, b0_{r+1}, 0, ..., b4_{r+1}, 0, 0, 0} -- every
+  // value a fast sample broadcasts into a packed f32 op on an even SGPR of one 16-dword scalar load
+  const float* tables_lv;
 };
+constexpr int kTabLvW = 16;   // floats per tables_lv window
 
 // rows per column: at least kTabTRows, so that k_episode_jl's chunk loads address their columns with
 // compile-time offsets from one base (no per-column 64-bit address arithmetic in the sample loop)

@@ -1014,15 +1014,18 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   // clamp and every row address of an unrolled block is a compile-time offset from one base.  With
   // the registered layout (ProMP, 5 basis functions: 8-float rows) the two pieces are contiguous,
   // row k + 2's floats 5..7 and row k + 3's 0..4: one 8-dword scalar load per sample.
+  cfloat_ptr lvtab = nullptr;   // tables_lv from the plan start row (wave-uniform)
   auto lv_load = [&](int k) {
     if constexpr (TrajT::KS == 8 && NBL == 5) {
-      typedef float f8u __attribute__((ext_vector_type(8), aligned(4)));
-      typedef const f8u __attribute__((address_space(4)))* cf8_ptr;
-      const f8u r = *(cf8_ptr)(tg.stab + (uint32_t)(k + 2) * 8u + 5u);
+      // window k + 2 of tables_lv: dt, 1 / dt of row k + 2 and the basis of row k + 3, each on an even
+      // SGPR (a packed f32 op broadcasts the low half of an aligned SGPR pair: no realigning moves)
+      typedef float f16u __attribute__((ext_vector_type(16), aligned(64)));
+      typedef const f16u __attribute__((address_space(4)))* cf16_ptr;
+      const f16u r = *(cf16_ptr)(lvtab + (uint32_t)(k + 2) * (uint32_t)kTabLvW);
       rdti = r[0];
-      rrdt = r[1];
+      rrdt = r[2];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) rb_[j] = r[3 + j];
+      for (int j = 0; j < 5; ++j) rb_[j] = r[4 + 2 * j];
     } else {
 #pragma unroll
       for (int j = 0; j < NBL; ++j) rb_[j] = tg.stab[(uint32_t)(k + 3) * TrajT::KS + j];
@@ -1180,6 +1183,7 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     const int s0u = __builtin_amdgcn_readfirstlane(s0);
     if (__ballot(s0 != s0u) != 0) fast_ok = false;
     if constexpr (MP != MP_GIVEN) tg.stab = (cfloat_ptr)(uintptr_t)s.tables + (size_t)s0u * tg.str();
+    if constexpr (LV) lvtab = (cfloat_ptr)(uintptr_t)s.tables_lv + (size_t)s0u * kTabLvW;
     // nfast full 8-blocks, then the remainder before the first sample that needs the generic
     // path (e.g. 192..198 ahead of step 199) as one partial block of np < 8 samples
     const int lim2_min = wave_min(lim2);
