@@ -402,7 +402,6 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_start = off; off = align_up(off + sizeof(double) * N);
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
   const size_t o_tabt = off; off = align_up(off + sizeof(float) * (size_t)tables_t_rows(h->dc.rows) * h->dc.stride);
-  const size_t o_tablv = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * kTabLvW);
   // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128, k_episode);
   // for the direct envs also k_episode_hp's candidate final states (2 (2 n_links + 1) rows, fgx_hp.h)
   const bool direct = cfg->env_kind != FGX_ENV_SIMPLE && cfg->mp_kind != FGX_MP_NONE;
@@ -427,7 +426,6 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   h->st.plan_len = nullptr;
   h->st.tables = h->tables;
   h->st.tables_t = (const float*)(b + o_tabt);
-  h->st.tables_lv = (const float*)(b + o_tablv);
   h->st.start = (double*)(b + o_start);
   (void)hipMemset(h->state_block, 0, off);
   if (h->learned()) {
@@ -462,11 +460,6 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
     const int n = tables_t_rows(d.rows) * d.stride;
     hipLaunchKernelGGL(k_tables_transpose, dim3((n + 255) / 256), dim3(256), 0, 0, d.rows, d.stride, d.nb, h->tables,
                        (float*)(b + o_tabt));
-    if (d.mp == MP_PROMP && d.nb == 5) {
-      const int nw = d.rows * kTabLvW;
-      hipLaunchKernelGGL(k_tables_lv, dim3((nw + 255) / 256), dim3(256), 0, 0, d.rows, d.stride, d.nb, h->tables,
-                         (float*)(b + o_tablv));
-    }
   }
   e = hipGetLastError();
   if (e != hipSuccess) { fgx_destroy(h); return fail(FGX_E_HIP, std::string("table kernel: ") + hipGetErrorString(e)); }

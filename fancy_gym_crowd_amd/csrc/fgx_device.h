@@ -119,20 +119,9 @@ struct DevState {
   // j * RT + r + tables_t_pad(j, nb) (k_episode_jl's ProMP chunks load 8 consecutive rows of one
   // column with one 32-byte-aligned scalar load)
   const float* tables_t;
-  // per-sample windows of the shared table for k_episode's level-scheduled ProMP samples (5 basis
-  // functions): window r = 16 floats {dt_r, 0, 1/dt_r, 0, b0_{r+1}, 0, ..., b4_{r+1}, 0, 0, 0} -- every
-  // value a fast sample broadcasts into a packed f32 op on an even SGPR of one 16-dword scalar load
-  const float* tables_lv;
 };
-constexpr int kTabLvW = 16;   // floats per tables_lv window
 
-// rows per column: at least kTabTRows, so that k_episode_jl's chunk loads address their columns with
-// compile-time offsets from one base (no per-column 64-bit address arithmetic in the sample loop)
-constexpr int kTabTRows = 512;
-__host__ __device__ inline int tables_t_rows(int rows) {
-  const int r = (rows + 32 + 7) & ~7;
-  return r > kTabTRows ? r : kTabTRows;
-}
+__host__ __device__ inline int tables_t_rows(int rows) { return (rows + 32 + 7) & ~7; }
 // basis columns start their rows at offset 6 (a chunk reads rows k0 + 2 ..), the dt columns at 7
 // (rows k0 + 1 ..): both land on multiples of 8 for k0 % 8 == 0
 __host__ __device__ inline int tables_t_pad(int col, int nb) { return col < nb ? 6 : 7; }

@@ -196,14 +196,12 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
 #pragma unroll
   for (int sl = 0; sl < SPW; ++sl) { A[sl] = -0.0; B[sl] = -0.0; Tl[sl] = 0.0; }   // -0.0 + r == r
   const int gr = g < G ? g : G - 1;   // idle lanes read (and discard) the last env's rows
-  // rows hold G NL columns; idle lanes write the rows' padding column XS - 1, which nothing reads, so
-  // the stores need no branch and the fast chunk stays one basic block (its f32 trajectory work can
-  // then be scheduled into the f64 recurrence's dependency stalls)
-  const int sq_col = (G * NL == 64 || lane < G * NL) ? lane : XS - 1;
   auto write_sq = [&](int ch, const double* sq) __attribute__((always_inline)) {
-    double* b = ex + (ch & 1) * (8 * XS) + sq_col;
+    double* b = ex + (ch & 1) * (8 * XS);
+    if (G * NL == 64 || lane < G * NL) {   // (rows hold G NL columns: idle lanes must not write)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) b[j * XS] = sq[j];
+      for (int j = 0; j < 8; ++j) b[j * XS + lane] = sq[j];
+    }
   };
   // sum_d a_d^2 in joint order, the reward 0 - ctrl (rdist = 0 below env step 199) and numpy's
   // pairwise slots, branch-free (selects); chunk ch < 0 changes nothing
@@ -269,15 +267,13 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   struct Cols { f8u b[NBL]; f8u dt, rd; };
   auto traj_load = [&](int k0, Cols& cl) __attribute__((always_inline)) {
     if constexpr (PKT) {
-      // the fast path runs only with the column length kTabTRows (fast_count): every column of the chunk
-      // is a compile-time offset from one base, one scalar address per chunk
-      constexpr int RT = kTabTRows;
-      const uint32_t R = (uint32_t)(s0u + k0);   // absolute row of sample k0: dt row R + 1, next basis row R + 2
-      const cfloat_ptr tt = (cfloat_ptr)(uintptr_t)s.tables_t + R + 8;
+      const int RT = tables_t_rows(c.rows);
+      const int R = s0u + k0;   // absolute row of sample k0: its dt row is R + 1, its next basis row R + 2
+      const cfloat_ptr tt = (cfloat_ptr)(uintptr_t)s.tables_t;
 #pragma unroll
-      for (int j = 0; j < NBL; ++j) cl.b[j] = *(cf8_ptr)(tt + j * RT);
-      cl.dt = *(cf8_ptr)(tt + NBL * RT);
-      cl.rd = *(cf8_ptr)(tt + (NBL + 1) * RT);
+      for (int j = 0; j < NBL; ++j) cl.b[j] = *(cf8_ptr)(tt + (size_t)j * RT + R + 8);
+      cl.dt = *(cf8_ptr)(tt + (size_t)NBL * RT + R + 8);
+      cl.rd = *(cf8_ptr)(tt + (size_t)(NBL + 1) * RT + R + 8);
     }
   };
   auto traj_fast = [&](int k0, const Cols& cl, float* Pt, float* Vt) __attribute__((always_inline)) {
@@ -419,7 +415,6 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   // 8 ch <= kfk) and, generic trajectories only, chunk ch + 1's samples are below T - 1 (8 ch + 16 < T)
   auto fast_count = [&](int nchunks) __attribute__((always_inline)) -> int {
     if (Lmin != Lmax || !nan_free) return 0;
-    if (PKT && tables_t_rows(c.rows) != kTabTRows) return 0;   // (traj_load's column offsets)
     const int L = Lmin;
     const int bend = __builtin_amdgcn_readlane(sg.bend, lead);
     const int kfk = __builtin_amdgcn_readlane(sg.k_fk, lead);

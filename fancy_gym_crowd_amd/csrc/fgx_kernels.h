@@ -1009,29 +1009,13 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
   constexpr int NLP = (NL + 1) / 2;
   float rb_[NBL];         // basis row k + 3 (trajectory of sample k + 1: its next position)
   float rdti = 0.0f, rrdt = 0.0f;   // dt and 1 / dt of row k + 2
-  // rows for the region of sample k: dt and 1 / dt of row k + 2, the basis of row k + 3.  The fast
-  // blocks only take waves whose reads stay inside the table (lv_ok below), so the row index needs no
-  // clamp and every row address of an unrolled block is a compile-time offset from one base.  With
-  // the registered layout (ProMP, 5 basis functions: 8-float rows) the two pieces are contiguous,
-  // row k + 2's floats 5..7 and row k + 3's 0..4: one 8-dword scalar load per sample.
-  cfloat_ptr lvtab = nullptr;   // tables_lv from the plan start row (wave-uniform)
-  auto lv_load = [&](int k) {
-    if constexpr (TrajT::KS == 8 && NBL == 5) {
-      // window k + 2 of tables_lv: dt, 1 / dt of row k + 2 and the basis of row k + 3, each on an even
-      // SGPR (a packed f32 op broadcasts the low half of an aligned SGPR pair: no realigning moves)
-      typedef float f16u __attribute__((ext_vector_type(16), aligned(64)));
-      typedef const f16u __attribute__((address_space(4)))* cf16_ptr;
-      const f16u r = *(cf16_ptr)(lvtab + (uint32_t)(k + 2) * (uint32_t)kTabLvW);
-      rdti = r[0];
-      rrdt = r[2];
+  int rmax = 0;           // last table row reachable through stab (wave-uniform)
+  auto lv_load = [&](int k) {   // rows for the region of sample k (clamped: never past the table)
+    const int rb = min(k + 3, rmax), rd = min(k + 2, rmax);
 #pragma unroll
-      for (int j = 0; j < 5; ++j) rb_[j] = r[4 + 2 * j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < NBL; ++j) rb_[j] = tg.stab[(uint32_t)(k + 3) * TrajT::KS + j];
-      rdti = tg.stab[(uint32_t)(k + 2) * TrajT::KS + NBL];
-      rrdt = tg.stab[(uint32_t)(k + 2) * TrajT::KS + NBL + 1];
-    }
+    for (int j = 0; j < NBL; ++j) rb_[j] = tg.stab[(size_t)rb * TrajT::KS + j];
+    rdti = tg.stab[(size_t)rd * TrajT::KS + NBL];
+    rrdt = tg.stab[(size_t)rd * TrajT::KS + NBL + 1];
   };
   auto lv_sample = [&](int k, auto Jtag, auto PHtag) {
     constexpr int J = decltype(Jtag)::value;
@@ -1183,20 +1167,19 @@ __device__ __forceinline__ void episode_body(const DevCfg& c, const DevState& s,
     const int s0u = __builtin_amdgcn_readfirstlane(s0);
     if (__ballot(s0 != s0u) != 0) fast_ok = false;
     if constexpr (MP != MP_GIVEN) tg.stab = (cfloat_ptr)(uintptr_t)s.tables + (size_t)s0u * tg.str();
-    if constexpr (LV) lvtab = (cfloat_ptr)(uintptr_t)s.tables_lv + (size_t)s0u * kTabLvW;
     // nfast full 8-blocks, then the remainder before the first sample that needs the generic
     // path (e.g. 192..198 ahead of step 199) as one partial block of np < 8 samples
     const int lim2_min = wave_min(lim2);
-    // LV: the last fast sample's look-ahead region reads row lim2_min + 3 (lv_load, unclamped): it
-    // must lie inside the table seen from the plan start (always, for Te <= T and rows >= s0 + T + 2)
-    if (LV && lim2_min + 3 > c.rows - 1 - s0u) fast_ok = false;
     const int nfast = fast_ok ? lim2_min / 8 : 0;
     const int np = fast_ok ? lim2_min % 8 : 0;
     if constexpr (MP != MP_GIVEN) {
       if (nfast > 0 || np > 0) {   // look-ahead of the first fast sample
         tg.template at<true, true>(c, 0, npos, nvel);
         pre = true;
-        if constexpr (LV) lv_load(0);
+        if constexpr (LV) {
+          rmax = c.rows - 1 - s0u;
+          lv_load(0);
+        }
       }
     }
     // Two loops: blocks before the pairwise split push into the level-1 sums a[] only, blocks from

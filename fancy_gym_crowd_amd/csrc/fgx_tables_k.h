@@ -52,17 +52,4 @@ __global__ void k_tables_transpose(int rows, int stride, int nb, const float* ta
   tt[i] = (r >= 0 && r < rows) ? tab[(size_t)r * stride + col] : 0.0f;
 }
 
-// tables_lv (DevState): window r of the ProMP rows' dt / 1/dt (columns nb, nb + 1) and row r + 1's basis
-// at even offsets; rows past the table read as 0 (never used)
-__global__ void k_tables_lv(int rows, int stride, int nb, const float* tab, float* lv) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows * kTabLvW) return;
-  const int r = i / kTabLvW, p = i - r * kTabLvW;
-  float v = 0.0f;
-  if (p == 0) v = tab[(size_t)r * stride + nb];
-  else if (p == 2) v = tab[(size_t)r * stride + nb + 1];
-  else if (p >= 4 && (p & 1) == 0 && (p - 4) / 2 < nb && r + 1 < rows) v = tab[(size_t)(r + 1) * stride + (p - 4) / 2];
-  lv[i] = v;
-}
-
 }  // namespace fgx
