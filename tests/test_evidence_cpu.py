@@ -13,8 +13,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from fancy_gym_crowd_amd import _build  # noqa: E402
 
-BENCH_LINE = os.path.join(ROOT, "profiles", "r05_bench_n1_final.json")
-KERNEL_STATS = os.path.join(ROOT, "profiles", "r05_kernel_stats_bench_final.csv")
+BENCH_LINE = os.path.join(ROOT, "profiles", "r06_bench_n1_final.json")
+KERNEL_STATS = os.path.join(ROOT, "profiles", "r06_kernel_stats_bench_final.csv")
 
 
 def _line():
@@ -26,7 +26,7 @@ def _current_or_skip(ids):
     """evidence of another build (sources changed since the PMC passes): nothing to check yet"""
     if ids != {_build.source_hash()}:
         pytest.skip(f"profiles are of build(s) {sorted(ids)}, the sources are {_build.source_hash()}: "
-                    "re-run tools/gpu_pmc_r03.sh and tools/gpu_final_r05.sh")
+                    "re-run tools/gpu_pmc_r03.sh and tools/gpu_final_r06.sh")
 
 
 def test_pmc_summary_is_of_this_tree():
@@ -66,7 +66,7 @@ def test_bench_roofline_recomputes_from_profiles():
 def test_pmc_summary_rebuilds_from_committed_csvs(tmp_path):
     out = tmp_path / "s.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"),
-                    os.path.join(ROOT, "profiles", "r05_pmc"), "--no-copy", "--out", str(out),
+                    os.path.join(ROOT, "profiles", "r06_pmc"), "--no-copy", "--out", str(out),
                     "--build-id", _build.source_hash()], check=True, capture_output=True)
     got = json.loads(out.read_text())["entries"]
     with open(bench.PMC_SUMMARY) as f:
@@ -106,3 +106,14 @@ def test_basis_gemm_accounting_from_pmc():
         g = bench.basis_gemm_fields(N, T, n, nb, n * nb, bg["us"] * 1e-6, pmc)
         for k in ("flops_algorithmic", "mfma_frac", "algorithmic_tflops", "hbm_GBps"):
             assert g[k] == pytest.approx(bg[k], rel=1e-9), k
+
+
+def test_cpu_baseline_calibration_committed():
+    """the CPU baseline worker bench.py runs on the GPU box is calibrated against the
+    shimmed reference loop on one core of the build container (tools/cpu_calibration.py)."""
+    import json
+    p = os.path.join(ROOT, "profiles", "r06_cpu_calibration.json")
+    d = json.load(open(p))
+    assert d["reference_steps_per_s"] > 0 and d["port_steps_per_s"] > 0
+    assert abs(d["port_over_reference"] - d["port_steps_per_s"] / d["reference_steps_per_s"]) < 1e-9
+    assert 0.2 < d["port_over_reference"] < 5.0
