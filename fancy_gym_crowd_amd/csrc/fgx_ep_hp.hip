@@ -33,6 +33,11 @@ static int launch_hp_ctrl(const DevCfg& c, const DevState& s, const float* param
                           std::string& err) {
   // per-step arrays: the INFO instantiation
   const bool info = o.positions || o.step_actions || o.step_obs || o.step_rewards || o.is_collided || o.end_effector;
+#ifdef FGX_HP_ONLY_CFG3   // diagnostics builds (tools/unit_variant.py): config 3's instantiation only
+  if (MP == MP_PRODMP && c.ctrl == CTRL_PD && !info) return launch_hp<MP_PRODMP, CTRL_PD, G, false>(c, s, params, o, stream, err);
+  err = "FGX_HP_ONLY_CFG3 build";
+  return -1;
+#endif
   switch (c.ctrl) {
     case CTRL_PD: return info ? launch_hp<MP, CTRL_PD, G, true>(c, s, params, o, stream, err)
                               : launch_hp<MP, CTRL_PD, G, false>(c, s, params, o, stream, err);

@@ -196,3 +196,48 @@ def test_hp_info_reward_aggregation(monkeypatch):
         monkeypatch.delenv("FGX_V2")
         for x, y in zip(ra[:4], rb[:4]):
             np.testing.assert_array_equal(np_(x), np_(y))
+
+
+def test_hp_fast_fk_near_thresholds(monkeypatch):
+    """info_level 0 takes the collision booleans from an error-bounded approximate FK and recomputes a
+    lane exactly where a decision is within its bound (fgx_hp.h: hp_fast_collision, hp_link_wall_rb).
+    Zero-velocity plans (ProMP, velocity controller, zero weights) hold each env at a pose built to sit
+    on a decision's threshold for the whole segment: arms lying within 1e-17 .. 1e-12 of the ground
+    (the wall test's skip rule and its end-point comparisons), links folded back to within 1e-13 ..
+    1e-11 rad (ccw values around the self-collision test's 1e-12), the collinear reset pose, squares
+    with touching segments; beside envs with random plans.  Bit-identical to k_episode."""
+    env_id, N = "fancy_ProMP/HoleReacher-v0", 1024
+    probe = fgx.make(env_id, num_envs=8, device=DEV, info_level=0)
+    P = probe.n_params
+    del probe
+    st = fgx.make(env_id, num_envs=N, device=DEV, info_level=0)
+    st.reset(seed=3)
+    q = np_(st.get_state()["q"]).copy()
+    del st
+    poses = [[np.pi / 2, 0, 0, 0, 0], [np.pi / 2, np.pi / 2, np.pi / 2, np.pi / 2, np.pi / 2],
+             [np.pi / 2, -np.pi / 2, -np.pi / 2, -np.pi / 2, -np.pi / 2]]
+    for t in (0.0, 1e-17, 1e-16, 4e-16, 1e-15, 3e-15, 1e-14, 3e-14, 1e-13, 1e-12):
+        for sgn in (1.0, -1.0):
+            poses.append([sgn * t, 0, 0, 0, 0])                    # along +x, just above / below the ground
+            poses.append([np.pi - sgn * t, 0, 0, 0, 0])            # along -x
+            poses.append([sgn * t, 0, 0, np.pi / 2, 0])            # three links on the ground, two rising
+    for dlt in (1e-13, 3e-13, 7e-13, 1e-12, 1.3e-12, 2e-12, 1e-11):
+        for sgn in (1.0, -1.0):
+            poses.append([np.pi / 2, sgn * (np.pi - dlt), 0, 0, 0])       # link 1 folded back onto link 0
+            poses.append([np.pi / 2, 0.3, sgn * (np.pi - dlt), 0, 0])
+            poses.append([np.pi / 2, 0, 0, sgn * (np.pi - dlt), sgn * dlt])
+    poses = np.array(poses)
+    n_pose = len(poses)
+    assert n_pose < N // 2
+    q[:n_pose] = poses
+    rng = np.random.default_rng(11)
+    plist = []
+    for b in range(2):
+        p = rng.standard_normal((N, P)).astype(np.float32)
+        p[:n_pose] = 0.0                      # zero velocity: the pose holds for every sample
+        plist.append(p)
+    a, tla = _steps(env_id, None, {}, N, 2, plist, True, monkeypatch, g=1, set_q=q)
+    b, tlb = _steps(env_id, None, {}, N, 2, plist, False, monkeypatch, set_q=q)
+    _same(a, b)
+    # the poses decide both ways: some collide at once, some hold for the whole segment
+    assert (tla[0][:n_pose] == 1).any() and (tla[0][:n_pose] == 200).any()
