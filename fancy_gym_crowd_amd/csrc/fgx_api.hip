@@ -403,10 +403,10 @@ int fgx_create(const fgx_config* cfg, int64_t n_envs, int device, void** handle)
   const size_t o_tab = off; off = align_up(off + sizeof(float) * (size_t)h->dc.rows * h->dc.stride + 16);
   const size_t o_tabt = off; off = align_up(off + sizeof(float) * (size_t)tables_t_rows(h->dc.rows) * h->dc.stride);
   // step rewards of one BB step for the exact pairwise return of terminating envs (L > 128, k_episode);
-  // for the direct envs also k_episode_hp's candidate final states (2 (2 n_links + 1) rows, fgx_hp.h)
+  // for the direct envs also k_episode_hp's candidate final states (2 consumers x 2 n_links rows, fgx_hp.h)
   const bool direct = cfg->env_kind != FGX_ENV_SIMPLE && cfg->mp_kind != FGX_MP_NONE;
   const bool need_rew = direct || (h->dc.sched_state && cfg->mp_kind != FGX_MP_NONE && h->dc.T > 128);
-  const size_t rew_rows = direct ? (size_t)std::max(h->dc.T, 2 * (2 * nl + 1)) : (size_t)h->dc.T;
+  const size_t rew_rows = direct ? (size_t)std::max(h->dc.T, 2 * (2 * nl)) : (size_t)h->dc.T;
   const size_t o_rew = off; off = align_up(off + (need_rew ? sizeof(double) * rew_rows * N : 0));
   e = hipMalloc(&h->state_block, off);
   if (e != hipSuccess) { delete h; return fail(FGX_E_NOMEM, std::string("hipMalloc state: ") + hipGetErrorString(e)); }

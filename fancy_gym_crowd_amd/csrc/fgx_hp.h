@@ -50,8 +50,8 @@ constexpr int kHpNS = 5;   // second-half starts s = 64, 72, ..., 96 of numpy's 
 constexpr int kHpS0 = 64;
 constexpr int kHpNR = 2;   // of them in the producer's registers (64, 72); the rest in LDS
 constexpr int kHpPA = 10;  // depth of the producer's acc_cost ring (its lead over the resolution + 8)
-// candidate final state rows per consumer in the handle's direct-env scratch: q, q̇, |ee - goal|^2
-template <int NL> __host__ __device__ constexpr int hp_cand_rows() { return 2 * NL + 1; }
+// candidate final state rows per consumer in the handle's direct-env scratch: q, q̇
+template <int NL> __host__ __device__ constexpr int hp_cand_rows() { return 2 * NL; }
 
 // LDS of one group (doubles): the q ring [buf][i][d][lane] and the action ring [buf][i][d][lane] (the
 // consumers' input: chunk it in buffer it & 1), the consumers' stop codes [buf][i][lane] (u8), the
@@ -73,177 +73,22 @@ struct HpLayout {
                        oFF = oBL + BL, oAL = oFF + FF, oSY = oAL + AL;
 };
 
-// The collision booleans of one sample (hole_reacher.py:126-179, base_reacher.py:105-119) from an
-// approximate FK, exactly equal to the exact path's (Env::fk + the wall and self-collision tests)
-// whenever `unsure` comes back false.  The exact path's joints J_k are sums of fgx_sincos (ocml) of the
-// cumulative angles; here each sincos is fgx_sincos_fast of the same (exactly summed) angle:
-//   * trig: |fast - exact| <= dT = 1e-15 per value for |angle| < 1e3 (fast: <= 2e-16 from the true
-//     value, tests/test_host_trig.py; ocml <= 1 ulp <= 2.2e-16);
-//   * joints: |J'_k - J_k| <= k (dT + ulp(5)) <= kE k per coordinate (each running sum rounds once
-//     in both paths, |sum| <= 5);
-//   * wall: a link is skipped by the exact path when both its end joints have y >= 0 (and the hole
-//     has a depth); y'_k >= kE k proves that, else the lane is unsure (0.3% of samples, the arm
-//     dipping below the ground: tools/hp_margins.py);
-//   * self-collision: each ccw value (classic_control/utils.py:1-2, "> 1e-12") of a segment pair
-//     (A B = link i, C D = link j) is a cross product of link directions u and joint differences:
-//     ccw(A,C,D) = P = cross(C - A, u_j), ccw(B,C,D) = P - R, ccw(A,B,C) = Q = cross(u_i, C - A),
-//     ccw(A,B,D) = Q + R with R = cross(u_i, u_j).  P', Q', R' computed from the approximate joints
-//     differ from the exact path's rounded reference-formula values by <= 1.7e-13 (the latter's own
-//     rounding on coordinates <= 5: <= 8.8e-14; the joints' and directions' errors: <= 7e-14); a
-//     decision is taken only outside [1e-12 - kM, 1e-12 + kM], kM = 3e-13.  At the reset pose (all
-//     links collinear) the values are ~0, far below the band.
-// A certain collision (|q| > pi with the self test on, or a pair certainly intersecting) decides the
-// sample whatever else is unsure.  |angle| >= 1e3, inf and NaN: unsure.
-constexpr double kHpE = 4e-15;   // per joint index (2x the bound above)
-constexpr double kHpM = 3e-13;
-
-// Env<NL>::link_wall (hole_reacher.py:126-179 for one link) on approximate link geometry: start joint
-// (bx, by) within eS of the exact path's, end joint within eE, direction (ck, sk) within 1e-15.  Equal
-// to the exact path's result whenever `unsure` stays false:
-//   * the end-point cases compare the end joints (p_0, p_99: the exact path's own joints) with the hole
-//     edges and the ground, each comparison taken only when the coordinate is farther than its error
-//     from the threshold;
-//   * the crossing cases use link_wall's index estimates only where they are `clear` (more than 1e-4
-//     from every integer: link_wall's proof bounds the estimate's error by 6e-5, and the approximate
-//     geometry moves the real crossing 99 (eE + 1e-15) / |k| <= 3e-9 more), which makes ceil(est) the
-//     first index of the exact points too; an estimate that is not clear (link_wall would evaluate
-//     points there) or an insane link (|k| < 1e-3, coordinates > 1e3) is unsure.
-__device__ __forceinline__ bool hp_link_wall_rb(double left, double right, double nd, double bx, double by,
-                                                double ck, double sk, double eS, double eE, bool& unsure) {
-  // a < t for a within e: 1 certainly, 0 certainly not, -1 unknown (and the same for a > t)
-  auto lt = [](double a, double t, double e) { return a < t - e ? 1 : (a >= t + e ? 0 : -1); };
-  auto gt = [](double a, double t, double e) { return a > t + e ? 1 : (a <= t - e ? 0 : -1); };
-  auto or2 = [](int a, int b) { return (a == 1 || b == 1) ? 1 : ((a == 0 && b == 0) ? 0 : -1); };
-  auto res = [&](int v) { unsure |= v < 0; return v == 1; };
-  const double x0 = bx, y0 = by, x1 = ck * 1.0 + bx, y1 = sk * 1.0 + by;
-  if (left <= right) {
-    const int l0 = lt(x0, left, eS), l1 = lt(x1, left, eE), r0 = gt(x0, right, eS), r1 = gt(x1, right, eE);
-    const int g0 = gt(x0, left, eS), g1 = gt(x1, left, eE), s0 = lt(x0, right, eS), s1 = lt(x1, right, eE);
-    if (l0 < 0 || l1 < 0 || r0 < 0 || r1 < 0 || g0 < 0 || g1 < 0 || s0 < 0 || s1 < 0) { unsure = true; return false; }
-    if ((l0 && l1) || (r0 && r1)) return res(or2(lt(y0, 0.0, eS), lt(y1, 0.0, eE)));
-    if (g0 && s0 && g1 && s1) return res(or2(lt(y0, nd, eS), lt(y1, nd, eE)));
-  }
-  // the crossing indices from link_wall's estimates (the same expressions), clear ones only
-  auto first = [&](float est, bool sane) {
-    const int je = (est > 0.0f) ? ((est < 100.0f) ? (int)__builtin_ceilf(est) : 100) : 0;
-    const float fr = est - __builtin_floorf(est);
-    const bool clear = sane && (est < -1.0f || est > 101.0f || (fr > 1e-4f && fr < 1.0f - 1e-4f));
-    unsure |= !clear;
-    return je;
-  };
-  const float rck = __builtin_amdgcn_rcpf((float)ck) * 99.0f, rsk = __builtin_amdgcn_rcpf((float)sk) * 99.0f;
-  auto cross = [](double t, double b, float r) { return (float)(t - b) * r; };
-  const bool tsane = __builtin_fabs(left) <= 1e3 && __builtin_fabs(right) <= 1e3 && __builtin_fabs(nd) <= 1e3;
-  const bool xsane = tsane && __builtin_fabs(ck) >= 1e-3 && __builtin_fabs(bx) <= 1e3;
-  const bool ysane = tsane && __builtin_fabs(sk) >= 1e-3 && __builtin_fabs(by) <= 1e3;
-  // {j : f(j) < t} / {j : f(j) > t} as [lo, hi); (a constant coordinate is insane: unsure)
-  auto below = [&](double dir, float est, bool sane, int& lo, int& hi) {
-    if (dir > 0.0) { lo = 0; hi = first(est, sane); }
-    else { lo = first(est, sane); hi = 100; }
-  };
-  auto above = [&](double dir, float est, bool sane, int& lo, int& hi) {
-    if (dir > 0.0) { lo = first(est, sane); hi = 100; }
-    else { lo = 0; hi = first(est, sane); }
-  };
-  int xl0, xl1, xr0, xr1, xL0, xL1, xR0, xR1, yg0, yg1, yd0, yd1;
-  const float el = cross(left, bx, rck), er = cross(right, bx, rck);
-  below(ck, el, xsane, xl0, xl1);    // px < left
-  above(ck, er, xsane, xr0, xr1);    // px > right
-  above(ck, el, xsane, xL0, xL1);    // px > left
-  below(ck, er, xsane, xR0, xR1);    // px < right
-  below(sk, cross(0.0, by, rsk), ysane, yg0, yg1);   // py < 0
-  below(sk, cross(nd, by, rsk), ysane, yd0, yd1);    // py < -depth
-  const bool c1 = max(xl0, yg0) < min(xl1, yg1);
-  const bool c2 = max(xr0, yg0) < min(xr1, yg1);
-  const bool c3 = max(max(xL0, xR0), yd0) < min(min(xL1, xR1), yd1);
-  return c1 || c2 || c3;
-}
-template <int NL>
-__device__ __forceinline__ bool hp_fast_collision(const double* rq, bool allow_self, bool allow_wall, double w_left,
-                                                  double w_right, double w_nd, bool& unsure, bool& walled) {
-  double ux[NL], uy[NL], Jx[NL + 1], Jy[NL + 1];
-  Jx[0] = 0.0; Jy[0] = 0.0;
-  bool lim = false, wall_hit = false, wall_unsure = false;
-  unsigned test = 0;
-  double A = 0.0, ang = 0.0, x = 0.0, y = 0.0;
-#pragma unroll
-  for (int d = 0; d < NL; ++d) {
-    const double qv = rq[d * 64];
-    lim |= __builtin_fabs(qv) > M_PI;
-    A += __builtin_fabs(qv);
-    ang = (d == 0) ? qv : ang + qv;
-    fgx_sincos_fast(ang, &uy[d], &ux[d]);
-    x = (d == 0) ? ux[d] : x + ux[d];
-    y = (d == 0) ? uy[d] : y + uy[d];
-    Jx[d + 1] = 0.0 + x;
-    Jy[d + 1] = 0.0 + y;
-    // the exact path skips the link when both end joints have y >= 0 (Env::wall_collision): certainly
-    // (bit d of `test` clear) when the approximate ones are above their errors
-    if (!allow_wall && !(Jy[d] >= kHpE * d && Jy[d + 1] >= kHpE * (d + 1) && w_nd <= 0.0)) test |= 1u << d;
-  }
-  // the links that need the wall test, one per lane and pass (rarely more than one pass: 0.3% of the
-  // samples have a link below the ground), with the link's values selected by index
-  walled = test != 0;
-  while (test) {
-    const int d = __builtin_ctz(test);
-    test &= test - 1;
-    double bx = Jx[0], by = Jy[0], ex = Jy[1], ck = ux[0], sk = uy[0];
-#pragma unroll
-    for (int k = 1; k < NL; ++k)
-      if (d == k) { bx = Jx[k]; by = Jy[k]; ex = Jy[k + 1]; ck = ux[k]; sk = uy[k]; }
-    const double eS = kHpE * d, eE = kHpE * (d + 1);
-    const bool may_skip = by >= -eS && ex >= -eE && w_nd <= 0.0;
-    bool u = false;
-    const bool h = hp_link_wall_rb(w_left, w_right, w_nd, bx, by, ck, sk, eS, eE, u);
-    // a certain hit counts only if the exact path certainly runs the test
-    if (!u && h && !may_skip) wall_hit = true;
-    else wall_unsure |= u || h;
-  }
-  bool hit = false, self_unsure = false;
-  if (!allow_self) {
-    hit = lim;
-    constexpr double tH = 1e-12 + kHpM, tL = 1e-12 - kHpM;
-#pragma unroll
-    for (int i = 0; i < NL; ++i)
-#pragma unroll
-      for (int j = i + 2; j < NL; ++j) {
-        const double wx = Jx[j] - Jx[i], wy = Jy[j] - Jy[i];
-        const double R = __builtin_fma(ux[i], uy[j], -(uy[i] * ux[j]));
-        const double P = __builtin_fma(wx, uy[j], -(wy * ux[j]));
-        const double Q = __builtin_fma(ux[i], wy, -(uy[i] * wx));
-        const double PB = P - R, QD = Q + R;
-        const bool a = P > tH, b = PB > tH, cc = Q > tH, dd = QD > tH;
-        const bool u = (a != (P > tL)) || (b != (PB > tL)) || (cc != (Q > tL)) || (dd != (QD > tL));
-        hit |= !u && (a != b) && (cc != dd);
-        self_unsure |= u;
-      }
-  }
-  hit |= wall_hit;
-  unsure = !hit && (wall_unsure || self_unsure || !(A < 1e3));
-  return hit;
-}
-
-// INFO: the verbose-2 per-step arrays (black_box_wrapper.py:184-189,218-227,244-249) as well: the
-// producer writes the plan rows (positions / velocities) as it evaluates them, and at each chunk's
-// resolution the rows that need the counted / not-counted decision (step_actions from the action ring,
-// step_rewards, step_observations — cos / sin of q through obs_trig_fast, DESIGN.md §4.9 — NaN after
-// trajectory_length); the consumers write the env info rows of their samples (end_effector, is_collided,
-// is_success); the producer pads those after trajectory_length once every wave has left the loop.
 // The chunk barrier of one group (its producer and two consumers) when a workgroup holds several
-// groups: a workgroup s_barrier would make every group wait for the slowest of the four each chunk
-// (profiles/r06_hp_stamps.jsonl: waves parked 17-45% of their loop there).  Each wave publishes its
-// arrival count in the group's LDS word after its own LDS accesses have completed, then polls until
-// the other two have arrived (LDS is one memory: a wave that sees the count reads the data written
-// before it).  Every wave of a group arrives at the same barriers (the loop exits on the group's own
-// alive mask, which all three read after the same barrier); the poll is bounded.
+// groups: a workgroup s_barrier makes every group wait each chunk for the slowest of the four (section
+// clocks, profiles/r06_hp_stamps.jsonl: the waves of a four-group workgroup parked 17-45% of their loop
+// there).  Each wave publishes its arrival count in the group's LDS word once its own LDS accesses have
+// completed, then polls until the other two have arrived (LDS is one memory: a wave that sees the count
+// reads the data written before it).  The three waves of a group arrive at the same barriers (the loop
+// exits on the group's own alive mask, which all three read after the same barrier); the poll is
+// bounded.
 __device__ __forceinline__ void hp_group_barrier(uint32_t* cnt, int role, uint32_t target) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(cnt + role, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   for (int spin = 0; spin < (1 << 24); ++spin) {
-    const uint32_t a = __hip_atomic_load(cnt + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t b = __hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t c = __hip_atomic_load(cnt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (__builtin_amdgcn_readfirstlane((int)(a >= target && b >= target && c >= target))) break;
+    bool all = true;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) all &= __hip_atomic_load(cnt + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target;
+    if (__builtin_amdgcn_readfirstlane((int)all)) break;
     __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");
@@ -264,12 +109,18 @@ __device__ __forceinline__ void hp_group_barrier(uint32_t* cnt, int role, uint32
 #define FGX_HP_PUT(i, v) do { } while (0)
 #endif
 
+// INFO: the verbose-2 per-step arrays (black_box_wrapper.py:184-189,218-227,244-249) as well: the
+// producer writes the plan rows (positions / velocities) as it evaluates them, and at each chunk's
+// resolution the rows that need the counted / not-counted decision (step_actions from the action ring,
+// step_rewards, step_observations — cos / sin of q through obs_trig_fast, DESIGN.md §4.9 — NaN after
+// trajectory_length); the consumers write the env info rows of their samples (end_effector, is_collided,
+// is_success); the producer pads those after trajectory_length once every wave has left the loop.
 template <int MP, int CTRL, int NL, int NB, int G, bool INFO>
 __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, const float* __restrict__ params,
                                                        Outputs o) {
   using Lay = HpLayout<NL>;
   constexpr bool F32 = (CTRL != CTRL_PD);
-#ifdef FGX_HP_NO_GSYNC   // (A/B) the workgroup barrier for every shape
+#ifdef FGX_HP_NO_GSYNC   // (A/B builds) the workgroup barrier for every shape
   constexpr bool GSYNC = false;
 #else
   constexpr bool GSYNC = G > 1;   // per-group chunk barriers (hp_group_barrier)
@@ -279,7 +130,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int g = w % G, role = w / G;   // role 0: producer, 1: consumer C0, 2: consumer C1
 #ifdef FGX_STAMPS
-  unsigned long long hp_bar = 0, hp_res = 0, hp_prod = 0, hp_fast = 0;
+  unsigned long long hp_bar = 0, hp_res = 0, hp_prod = 0;
   const unsigned long long hp_t0 = __builtin_readcyclecounter();
 #endif
   double* gr = lds_hp + (size_t)g * Lay::GROUP;
@@ -308,7 +159,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
     if (role == 0 && lane < 3) ((uint32_t*)(gr + Lay::oSY))[lane] = 0u;
   }
   __syncthreads();
-  // the loop ends when no env of the group (GSYNC: of this group; else of the workgroup) is alive
+  // the loop ends when no env of the group (GSYNC; else of the workgroup) is alive
   auto all_done = [&](int rp) __attribute__((always_inline)) {
     uint64_t any = 0;
     if constexpr (GSYNC) {
@@ -321,26 +172,21 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
   };
   uint32_t* sy = (uint32_t*)(gr + Lay::oSY);
   auto chunk_barrier = [&](int it) __attribute__((always_inline)) {
+    FGX_HP_CLK(tb);
     if constexpr (GSYNC) hp_group_barrier(sy, role, (uint32_t)(it + 1));
     else lds_barrier();
+    FGX_HP_BAR(tb);
   };
 
   if (role != 0) {
     // ================================================================ consumers
     const int ci = role - 1;   // sample k = 2 c + ci of chunk c
-#ifdef FGX_HP_PRIO_C1   // (A/B) issue priority of the consumers over the producer
-    if (ci == 1) __builtin_amdgcn_s_setprio(FGX_HP_PRIO_C1);
-    else __builtin_amdgcn_s_setprio(FGX_HP_PRIO_C0);
-#endif
     const double gx = s.goal[e], gy = s.goal[N + e];
     // the wall's edges (Env::wall_collision: left / right of the hole, its depth below the ground)
     const double hx = s.hole[e], hw = s.hole[N + e], hd = s.hole[2 * N + e];
     const double w_left = hx - hw / 2, w_right = hx + hw / 2, w_nd = -hd;
     const bool allow_self = c.allow_self != 0, allow_wall = c.allow_wall != 0;
     bool own_done = false;   // this consumer saw a stop sample of the env: the segment ends there or earlier
-#ifdef FGX_HP_DIAG
-    long long n_walled = 0, n_unsure = 0;
-#endif
     for (int it = 0;; ++it) {
       const int rp = (it + 1) & 1;
       if (all_done(rp) || it > itmax) break;
@@ -349,65 +195,43 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
       const bool alive = ((al[rp] >> lane) & 1) && !own_done;
       if (it >= 1 && alive && k < Lst) {
         const double* rq = gr + Lay::oRQ + (size_t)((cpk & 1) * 2 + ci) * NL * 64;
-        double jx[NL + 1], jy[NL + 1];   // (INFO: the exact joints, the end effector's rows)
-        double c0q = 0.0, s0q = 0.0;     // (INFO: cos / sin of q[0], the observation's)
-        // the exact tests: FK (base_reacher.py:95-103, Env::fk's operations) fused with the wall test
-        // of each link as soon as its start joint and direction exist (hole_reacher.py:126-179,
-        // Env::wall_collision's per-link test), then the self-collision test (base_reacher.py:105-119);
-        // q is read from the ring as it is needed
-        auto exact_collision = [&]() __attribute__((always_inline)) {
-          jx[0] = 0.0; jy[0] = 0.0;
-          bool lim = false, wc = false;
-          double ang = 0.0, x = 0.0, y = 0.0;
+        // FK (base_reacher.py:95-103, Env::fk's operations) fused with the wall test of each link as
+        // soon as its start joint and direction exist (hole_reacher.py:126-179, Env::wall_collision's
+        // per-link test): only the joint positions stay live for the self-collision test
+        // (base_reacher.py:105-119); q is read from the ring as it is needed
+        double jx[NL + 1], jy[NL + 1];
+        jx[0] = 0.0; jy[0] = 0.0;
+        bool lim = false, wc = false;
+        double ang = 0.0, x = 0.0, y = 0.0;
+        double c0q = 0.0, s0q = 0.0;   // cos / sin of q[0] (the observation's)
 #pragma unroll
-          for (int d = 0; d < NL; ++d) {
-            const double qv = rq[d * 64 + lane];
-            lim |= __builtin_fabs(qv) > M_PI;   // base_reacher.py:38-39,111 (q > pi or q < -pi)
-            ang = (d == 0) ? qv : ang + qv;
-            double sn, cs;
-            fgx_sincos(ang, &sn, &cs);
-            if (d == 0) { c0q = cs; s0q = sn; }
-            x = (d == 0) ? cs : x + cs;
-            y = (d == 0) ? sn : y + sn;
-            jx[d + 1] = 0.0 + x;
-            jy[d + 1] = 0.0 + y;
-            if (!allow_wall && !(jy[d] >= 0.0 && jy[d + 1] >= 0.0 && w_nd <= 0.0))
-              wc |= Env<NL>::link_wall(w_left, w_right, w_nd, jx[d], jy[d], cs, sn);
-          }
-          bool sc = false;
-          if (!allow_self) {
-            sc = lim;
-#pragma unroll
-            for (int i = 0; i < NL; ++i)
-#pragma unroll
-              for (int j = i + 2; j < NL; ++j)
-                sc |= (ccw(jx[i], jy[i], jx[j], jy[j], jx[j + 1], jy[j + 1]) !=
-                       ccw(jx[i + 1], jy[i + 1], jx[j], jy[j], jx[j + 1], jy[j + 1])) &&
-                      (ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j], jy[j]) !=
-                       ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j + 1], jy[j + 1]));
-          }
-          return sc || wc;   // hr_simple_reward.py:19-53
-        };
-        bool coll;
-        if constexpr (INFO) {
-          coll = exact_collision();   // the rows need the exact joints of every sample
-        } else {
-          // info_level 0: the joints feed only the collision booleans, taken from the error-bounded
-          // approximate FK where it decides them (hp_fast_collision) and exactly where it cannot
-          bool unsure, walled;
-#ifdef FGX_STAMPS
-          const unsigned long long tf0 = __builtin_readcyclecounter();
-#endif
-          coll = hp_fast_collision<NL>(rq + lane, allow_self, allow_wall, w_left, w_right, w_nd, unsure, walled);
-#ifdef FGX_STAMPS
-          hp_fast += __builtin_readcyclecounter() - tf0;
-#endif
-#ifdef FGX_HP_DIAG   // diagnostics builds: wave-samples that ran the wall test / the exact fallback
-          n_walled += __ballot(walled) != 0;
-          n_unsure += __ballot(unsure) != 0;
-#endif
-          if (unsure) coll = exact_collision();
+        for (int d = 0; d < NL; ++d) {
+          const double qv = rq[d * 64 + lane];
+          lim |= qv > M_PI || qv < -M_PI;   // base_reacher.py:38-39,111
+          ang = (d == 0) ? qv : ang + qv;
+          double sn, cs;
+          fgx_sincos(ang, &sn, &cs);
+          if (d == 0) { c0q = cs; s0q = sn; }
+          x = (d == 0) ? cs : x + cs;
+          y = (d == 0) ? sn : y + sn;
+          jx[d + 1] = 0.0 + x;
+          jy[d + 1] = 0.0 + y;
+          if (!allow_wall && !(jy[d] >= 0.0 && jy[d + 1] >= 0.0 && w_nd <= 0.0))
+            wc |= Env<NL>::link_wall(w_left, w_right, w_nd, jx[d], jy[d], cs, sn);
         }
+        bool sc = false;
+        if (!allow_self) {
+          sc = lim;
+#pragma unroll
+          for (int i = 0; i < NL; ++i)
+#pragma unroll
+            for (int j = i + 2; j < NL; ++j)
+              sc |= (ccw(jx[i], jy[i], jx[j], jy[j], jx[j + 1], jy[j + 1]) !=
+                     ccw(jx[i + 1], jy[i + 1], jx[j], jy[j], jx[j + 1], jy[j + 1])) &&
+                    (ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j], jy[j]) !=
+                     ccw(jx[i], jy[i], jx[i + 1], jy[i + 1], jx[j + 1], jy[j + 1]));
+        }
+        const bool coll = sc || wc;   // hr_simple_reward.py:19-53
         const bool stop = coll || k == Lst - 1;
         if constexpr (INFO) {
           // the per-step rows of this sample (black_box_wrapper.py:218-227; the producer rewrites the last
@@ -467,8 +291,7 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
         }
         rs[((cpk & 1) * 2 + ci) * 64 + lane] = (uint8_t)((stop ? 1 : 0) | (coll ? 2 : 0));
         if (stop) {
-          // a candidate final state: this sample ends the segment unless an earlier one does; with the
-          // distance term of the reward at a collision or at env step 199 (hr_simple_reward.py:33-45)
+          // a candidate final state: this sample ends the segment unless an earlier one does
           const double* ra = gr + Lay::oRA + (size_t)((cpk & 1) * 2 + ci) * NL * 64;
           double* cd = cand + (int64_t)(ci * CR) * N + e;
 #pragma unroll
@@ -476,26 +299,16 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
             cd[(int64_t)d * N] = rq[d * 64 + lane];
             cd[(int64_t)(NL + d) * N] = ra[d * 64 + lane];
           }
-          if constexpr (INFO) {
-            const double dist = norm2(jx[NL] - gx, jy[NL] - gy);
-            cd[(int64_t)(2 * NL) * N] = dist * dist;
-          }
           own_done = true;
         }
       }
-      FGX_HP_CLK(tb);
       chunk_barrier(it);
-      FGX_HP_BAR(tb);
     }
-#ifdef FGX_HP_DIAG
-    count_inner(o.inner_steps, n_walled * 1000000 + n_unsure, lane == 0);
-#endif
 #ifdef FGX_STAMPS
     FGX_HP_PUT(0, hp_t0);
     FGX_HP_PUT(1, __builtin_readcyclecounter());
     FGX_HP_PUT(8, hp_bar);
     FGX_HP_PUT(10, (unsigned long long)role);
-    FGX_HP_PUT(11, hp_fast);
 #endif
     // the candidate states and this wave's rows complete before the producer reads the former and
     // overwrites rows past trajectory_length (a workgroup barrier does not wait for stores)
@@ -667,21 +480,19 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
         if (F32) flags |= 1u;
       }
     }
-    FGX_HP_CLK(tb);
 #ifdef FGX_STAMPS
-    hp_prod += tb - tr1;
+    hp_prod += __builtin_readcyclecounter() - tr1;
 #endif
     chunk_barrier(it);
-    FGX_HP_BAR(tb);
   }
 #ifdef FGX_STAMPS
   FGX_HP_PUT(0, hp_t0);
   FGX_HP_PUT(1, __builtin_readcyclecounter());
   FGX_HP_PUT(8, hp_bar);
   FGX_HP_PUT(9, (unsigned long long)it_end);
+  FGX_HP_PUT(10, 0ull);
   FGX_HP_PUT(11, hp_res);
   FGX_HP_PUT(12, hp_prod);
-  FGX_HP_PUT(10, 0ull);
 #endif
   if constexpr (INFO) {
     // the rest of every env's plan (black_box_wrapper.py:245-246: the full desired trajectory); the
@@ -714,17 +525,14 @@ __global__ __launch_bounds__(192 * G) void k_episode_hp(DevCfg c, DevState s, co
   const bool special = term || steps0 + L - 1 == 199;
   double dist2 = 0.0;
   if (special) {
-    if constexpr (INFO) {
-      dist2 = cd[(int64_t)(2 * NL) * N];   // (the consumer's exact joints)
-    } else {
-      // |ee - goal|^2 of the final state: the exact FK (Env::fk), once per env
-      Env<NL> f;
+    // |ee - goal|^2 of the final state (the consumer's candidate): Env::fk once per env rather than at
+    // every stop sample a consumer meets (one lane's stop costs the whole wave the branch)
+    Env<NL> f;
 #pragma unroll
-      for (int d = 0; d < NL; ++d) f.q[d] = cd[(int64_t)d * N];
-      f.fk();
-      const double dist = norm2(f.jx[NL] - s.goal[e], f.jy[NL] - s.goal[N + e]);
-      dist2 = dist * dist;
-    }
+    for (int d = 0; d < NL; ++d) f.q[d] = cd[(int64_t)d * N];
+    f.fk();
+    const double dist = norm2(f.jx[NL] - s.goal[e], f.jy[NL] - s.goal[N + e]);
+    dist2 = dist * dist;
   }
   const double rfin = special ? __builtin_fma(term ? 1.0 : 0.0, -pen, __builtin_fma(acc_l, -5e-8, dist2 * -1.0))
                               : acc_l * -5e-8;

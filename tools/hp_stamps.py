@@ -2,7 +2,7 @@
 
   FGX_LIB=tools/ab/libfgx_stamps.so python tools/hp_stamps.py [envs] [G]
 
-Row blockIdx * 3 G + w of the stamp buffer: 0 loop start, 1 loop end (shader clock), 8 cycles waiting
+Row blockIdx * (1 + NC) G + w of the stamp buffer: 0 loop start, 1 loop end (shader clock), 8 cycles waiting
 at the chunk barriers, 9 the producer's iteration count, 10 the role (0 producer, 1 / 2 consumers),
 11 / 12 the producer's resolve / produce cycles (consumers: 11 the cycles in hp_fast_collision).
 Prints one JSON line per role: median loop cycles, barrier cycles, their ratio.
@@ -39,13 +39,14 @@ lib = _lib.load()
 fn = lib.fgx_dbg_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-W = (N + 64 * G - 1) // (64 * G) * 3 * G
+NW = 3   # waves per group: producer, C0, C1
+W = (N + 64 * G - 1) // (64 * G) * NW * G
 buf = np.zeros(W * 16, dtype=np.uint64)
 assert fn(buf.ctypes.data, W * 16) == 0
 st = buf.reshape(W, 16).astype(np.int64)
-role = np.arange(W) % (3 * G) // G
+role = np.arange(W) % (NW * G) // G
 loop = st[:, 1] - st[:, 0]
-for r, name in enumerate(("producer", "consumer0", "consumer1")):
+for r, name in enumerate(("producer", "consumer0", "consumer1")[:NW]):
     m = role == r
     print(json.dumps({"envs": N, "G": G, "role": name, "waves": int(m.sum()),
                       "loop_cycles_median": int(np.median(loop[m])), "barrier_cycles_median": int(np.median(st[m, 8])),
