@@ -8,6 +8,17 @@
 #include <cstdlib>
 
 namespace {
+int jl_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return cus;
+  }();
+  return n;
+}
+
 template <int MP, int NL, int NB, int HLP = 0>
 int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params, const fgx::Outputs& o,
               hipStream_t stream, std::string& err) {
@@ -22,8 +33,13 @@ int launch_jl(const fgx::DevCfg& c, const fgx::DevState& s, const float* params,
   if (const char* v = std::getenv("FGX_JL_GW")) gw = std::max(1, std::min(S::G, std::atoi(v)));   // experiments
   const int64_t per_block = (int64_t)S::WAVES * gw;
   const unsigned blocks = (unsigned)((c.N + per_block - 1) / per_block);
-  hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB, HLP>), dim3(blocks), dim3(S::THREADS), S::lds_bytes(), stream, c,
-                     s, params, o, gw);
+  // the reset wave (fgx_jl.h) while every workgroup has a CU of its own (the 8-GPU shard: 8192 envs
+  // 23.8-24.0 -> 21.9-22.2 us, config 2 22.4 -> 20.1 us); past that its fifth wave costs a workgroup
+  // slot per CU (32768 envs 45.2 -> 48.2 us, profiles/r06_jl_resetwave_ab.log).  FGX_JL_RW=0 / 1: A/B
+  int rw = (!HLP && blocks <= (unsigned)jl_cus()) ? 1 : 0;
+  if (const char* v = std::getenv("FGX_JL_RW")) rw = (!HLP && v[0] == '1') ? 1 : 0;
+  hipLaunchKernelGGL((fgx::k_episode_jl<MP, NL, NB, HLP>), dim3(blocks), dim3(S::THREADS + 64 * rw), S::lds_bytes(),
+                     stream, c, s, params, o, gw, rw);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { err = std::string("k_episode_jl launch: ") + hipGetErrorString(e); return -2; }
   return 0;

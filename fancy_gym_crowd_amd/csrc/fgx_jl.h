@@ -45,6 +45,9 @@ struct JlShape {
   static constexpr int EPB = G * WAVES;         // envs per workgroup
   static constexpr int SPW = (8 + NL - 1) / NL; // pairwise slots owned per lane
   static constexpr int THREADS = 64 * WAVES * (HLP ? 2 : 1);
+  // the plain form may add a reset wave after the joint waves (kernel argument rw): the workgroup's
+  // VectorEnv auto-resets, run while the joint waves run their episodes
+  static constexpr int MAXT = THREADS + (HLP ? 0 : 64);
   // gathered f64 per env: A, B, tail (8 each), cfk, q, qd, then cos / sin of the cumulative angles
   // (FK) and of every q (observation), then the env's stored steps, plan count, flags and goal
   static constexpr int GX = 25 + 6 * NL;
@@ -87,16 +90,20 @@ struct JlShape {
 // the joint wave continues exactly as k_episode_jl (slow chunks, NaN re-run, gather, epilogue), the
 // helper wave's threads running the auto-resets of the split group.  Same operations in the same
 // order: bit-identical.
+//
+// rw (plain form, host-chosen): the workgroup has a fifth wave, the reset wave, which runs the
+// auto-resets from the launch on (below); otherwise the reset group after the gather does.
 template <int MP, int NL, int NB, int HLP = 0>
-__global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevCfg c, DevState s,
-                                                                         const float* __restrict__ params,
-                                                                         Outputs o, int gw) {
+__global__ __launch_bounds__((JlShape<NL, HLP>::MAXT)) void k_episode_jl(DevCfg c, DevState s,
+                                                                       const float* __restrict__ params,
+                                                                       Outputs o, int gw, int rw) {
   using S = JlShape<NL, HLP>;
   constexpr int G = S::G, EPB = S::EPB, SPW = S::SPW;
   constexpr int NBL = NB > 0 ? NB : 1;
   extern __shared__ double lds_jl[];
   const int lane = threadIdx.x & 63;
   const bool helper = HLP && (int)(threadIdx.x >> 6) >= S::WAVES;
+  const bool rwave = !HLP && rw && (int)(threadIdx.x >> 6) == S::WAVES;
   const int w = helper ? (int)(threadIdx.x >> 6) - S::WAVES : (int)(threadIdx.x >> 6);
   constexpr int XS = S::XS;
   double* ex = lds_jl + w * (16 * XS);  // this wave's two chunk buffers: a^2 of sample j at [j * XS + lane]
@@ -108,13 +115,65 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   const int64_t e = valid ? e0 : N - 1;   // clamped: loads stay in bounds, nothing is stored
   const uint64_t vmask = __ballot(valid);
   // diagnostics build: stamp slot of this wave (the helper's: none)
-  const int64_t wst = helper ? (int64_t)16384 * 64 : ((int64_t)blockIdx.x * S::WAVES + w) * 64;
+  const int64_t wst = (helper || rwave) ? (int64_t)16384 * 64 : ((int64_t)blockIdx.x * S::WAVES + w) * 64;
   FGX_STAMP(o, wst, 6);
   FGX_STAMP(o, wst, 0);
+
+  // ---- the reset wave (plain form): the VectorEnv auto-reset of every env of the workgroup whose
+  // segment ends in truncation (SimpleReacher never terminates).  It depends only on the env's PCG64
+  // stream, start angle and segment words -- all known before the episode -- so it runs from the
+  // launch on, beside the joint waves (section clocks: as the epilogue's reset group after the
+  // gather it was the launch's last ~7.7 k cycles, profiles/r03_stamps_s17.jsonl).  Its inputs are
+  // read first; it writes the env state only after the barrier by which every joint wave holds its
+  // env's state (q, q̇, segment words, goal) in registers.  It then leaves: the joint waves' later
+  // barriers wait on the surviving waves only.
+  if constexpr (!HLP) {
+    if (rwave) {
+      constexpr int NR = (EPB + 63) / 64;
+      bool rdo[NR];
+      int64_t rer[NR];
+      Pcg64 rgs[NR];
+      double rsp[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int t1 = lane + 64 * i, tw1 = t1 / G, tg1 = t1 - tw1 * G;
+        rer[i] = (int64_t)blockIdx.x * (S::WAVES * gw) + tw1 * gw + tg1;
+        rdo[i] = o.autoreset && t1 < EPB && tg1 < gw && rer[i] < N;
+        if (rdo[i]) {
+          JpSeg sr;
+          sr.init(c, s, rer[i], true);
+          rdo[i] = sr.steps + sr.L >= c.max_steps;
+        }
+        rsp[i] = 0.0;
+        if (rdo[i]) {
+          rgs[i] = load_rng(s.rng, N, rer[i]);
+          rsp[i] = s.start[rer[i]];
+        }
+      }
+      __syncthreads();   // R: the joint waves' env state is in their registers
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        if (rdo[i]) {
+          const int64_t er = rer[i];
+          Env<NL> vr;
+          if (!c.random_start) vr.sp = rsp[i];
+          vr.reset(c, rgs[i], false, 0);
+          store_rng(s.rng, N, er, rgs[i]);
+          if (c.random_start) s.start[er] = vr.sp;
+          emit_obs(c, vr, c.return_context, o.obs + er * c.out_dim, nullptr, true);
+          store_env(c, s, er, vr, false);   // SimpleReacher: no hole / reward state
+          s.plans[er] = 0;
+        }
+      }
+      return;
+    }
+  }
 
   // the joint's state first: its loads need nothing the segment computes (they are in flight while
   // the segment's loads return and its wave reductions run)
   double q = s.q[d * N + e], qd = s.qd[d * N + e];
+  const double q_in = q, qd_in = qd;   // (a NaN re-run restarts from these: the reset wave may have
+                                       // overwritten the stored state by then)
   // ---- the env's segment; wave-uniform bounds over the valid lanes
   JpSeg sg;
   sg.init(c, s, e, valid);
@@ -143,6 +202,10 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
       tg.init(c, pe + d * nb, s.tables, s0, &ic_q, &ic_qd, c.T, c.tau32, c.rcp_tau32, NL * nb + d - d * nb);
   };
   init_traj();
+  double gx = 0.0, gy = 0.0;   // the env's goal, for the return thread (FK reward, observation)
+  if (d == 0) { gx = s.goal[e]; gy = s.goal[N + e]; }
+  if constexpr (!HLP)
+    if (rw) __syncthreads();   // R: the reset wave may overwrite the env state after this
   FGX_STAMP(o, wst, 13);
   // basis rows through scalar loads when every valid lane's plan starts on the same row
   const int s0u = __builtin_amdgcn_readlane(s0, lead);
@@ -604,8 +667,8 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   };
   // the segment from its start state (re-run after a NaN control)
   auto restart = [&]() __attribute__((always_inline)) {
-    q = s.q[d * N + e];
-    qd = s.qd[d * N + e];
+    q = q_in;
+    qd = qd_in;
     init_traj();
     tg.stab = stab;
     cfk = 0.0;
@@ -634,14 +697,13 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
   }
 
   FGX_STAMP(o, wst, 3);
-  double gx = 0.0, gy = 0.0;   // the env's goal, for the return thread (FK reward, observation)
-  if (d == 0) { gx = s.goal[e]; gy = s.goal[N + e]; }
-  // The VectorEnv auto-reset of a truncated env depends only on its PCG64 stream and start angle,
-  // not on the episode: when the workgroup has a second group of EPB threads (R0 = EPB rounded up to
-  // whole waves), those threads run the resets concurrently with the first group's returns and
-  // final observations.  Their inputs are loaded here, so that the loads land under the gather.
+  // The helper form (no reset wave): the VectorEnv auto-reset of a truncated env depends only on its
+  // PCG64 stream and start angle, not on the episode: when the workgroup has a second group of EPB
+  // threads (R0 = EPB rounded up to whole waves), those threads run the resets concurrently with the
+  // first group's returns and final observations.  Their inputs are loaded here, so that the loads
+  // land under the gather.
   constexpr int R0 = (EPB + 63) / 64 * 64;
-  constexpr bool SPLIT = R0 + EPB <= S::THREADS;
+  const bool SPLIT = !rw && R0 + EPB <= S::THREADS;
   const int t1 = (int)threadIdx.x - R0, tw1 = t1 / G, tg1 = t1 - tw1 * G;
   const int64_t er = (int64_t)blockIdx.x * (S::WAVES * gw) + tw1 * gw + tg1;
   const bool rgrp = SPLIT && o.autoreset && t1 >= 0 && t1 < EPB && tg1 < gw && er < N;
@@ -777,7 +839,7 @@ __global__ __launch_bounds__((JlShape<NL, HLP>::THREADS)) void k_episode_jl(DevC
     if (j < ntail) res = res + ((fk_last && j == ntail - 1) ? r_fk : ga[(3 * j + 2) * EPB + t]);
   if (L > 128) res = PairwiseSum::comb(sa) + res;
   const bool trunc = v.steps >= c.max_steps;
-  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_, SPLIT);
+  episode_epilogue(c, s, o, et, v, st.plans, L, res, false, trunc, false, oc, os_, SPLIT || rw);
   FGX_STAMP(o, wst, 5);
   FGX_STAMP(o, wst, 7);
 }

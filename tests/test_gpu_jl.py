@@ -136,16 +136,21 @@ def test_jl_inner_steps_counter(kern):
             os.environ["FGX_EPISODE_KERNEL"] = old
 
 
-@pytest.mark.parametrize("N", [1000, 8192])
-def test_jl_equals_classic_split_autoreset(N, monkeypatch):
-    """The auto-reset of truncated envs runs on a second thread group of each jl workgroup, beside the
-    returns / final observations of the first (fgx_jl.h epilogue): random_start False (the start
-    angle is restored, base_reacher.py:77-93) with envs at every env step, so only some envs of a
-    workgroup truncate; jl and k_episode agree bit for bit, state included."""
+@pytest.mark.parametrize("rw", ["auto", "0", "1"])
+@pytest.mark.parametrize("N", [1000, 8192, 32768])
+def test_jl_equals_classic_split_autoreset(N, rw, monkeypatch):
+    """The auto-reset of truncated envs runs on each jl workgroup's reset wave, beside the joint waves'
+    episodes (fgx_jl.h: it overwrites the env state once every joint wave holds it in registers), or
+    (FGX_JL_RW=0, and by default past one workgroup per CU) on the reset group after the gather:
+    random_start False (the start angle is restored, base_reacher.py:77-93) with envs at every env
+    step, so only some envs of a workgroup truncate; jl and k_episode agree bit for bit, state
+    included."""
     env_id = "fancy_ProMP/LongSimpleReacher-v0"
     rng = np.random.default_rng(91)
     params = [rng.standard_normal((N, 25), dtype=np.float32) for _ in range(3)]
     outs = []
+    if rw != "auto":
+        monkeypatch.setenv("FGX_JL_RW", rw)
     for kern in ("jl", "classic"):
         monkeypatch.setenv("FGX_EPISODE_KERNEL", kern)
         env = fgx.make(env_id, num_envs=N, device=DEV, info_level=0, random_start=False)
