@@ -362,6 +362,16 @@ if __name__ == "__main__":
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
     if "trajrun" in which:
         traj_run_scan()
+    if "dmpshape" in which:   # k_traj_run DMP: fewer envs per group for longer pieces (whole runs at GE <= 3)
+        for _ in range(2):
+            for ge, rc in (("12", "40"), ("6", "80"), ("6", "100"), ("4", "200"), ("3", "200"), ("2", "200")):
+                for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT"):
+                    os.environ.pop(k, None)
+                os.environ.update({"FGX_TRAJ_GE": ge, "FGX_TRAJ_RC": rc, "FGX_TRAJ_NT": "1"})
+                trajectory("fancy_DMP/LongSimpleReacher-v0", 65536)
+        for k in ("FGX_TRAJ_GE", "FGX_TRAJ_RC", "FGX_TRAJ_NT"):
+            os.environ.pop(k, None)
+        trajectory("fancy_DMP/LongSimpleReacher-v0", 65536)
     if "dmp" in which:   # DMP trajectory: the default shape against explicit ones
         for kv in ({}, {"FGX_TRAJ_GE": "6"}, {"FGX_TRAJ_GE": "8"}, {"FGX_TRAJ_GE": "10"},
                    {"FGX_TRAJ_RC": "32"}, {"FGX_TRAJ_GE": "8", "FGX_TRAJ_RC": "32"}, {}):
