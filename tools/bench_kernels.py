@@ -362,6 +362,9 @@ if __name__ == "__main__":
             trajectory("fancy_ProDMP/HoleReacher-v0", 65536, force)
     if "trajrun" in which:
         traj_run_scan()
+    if "config3" in which:   # k_episode_hp at four (65536) and one (32768) groups per workgroup
+        episode("fancy_ProDMP/HoleReacher-v0", 65536, label="config3: ProDMP HoleReacher", reps=10)
+        episode("fancy_ProDMP/HoleReacher-v0", 32768, label="config3 half: ProDMP HoleReacher", reps=10)
     if "dmpshape" in which:   # k_traj_run DMP: fewer envs per group for longer pieces (whole runs at GE <= 3)
         for _ in range(2):
             for ge, rc in (("12", "40"), ("6", "80"), ("6", "100"), ("4", "200"), ("3", "200"), ("2", "200")):
